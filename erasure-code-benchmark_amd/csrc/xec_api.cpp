@@ -1,0 +1,199 @@
+// xec_api.cpp -- the C ABI of libxec_hip.so (declared in include/xec.h).
+//
+// Host-side responsibilities, each following the reference behaviour:
+//   - initialisation contract        xorec_gpu_cmp.cu:7-27, xorec.cpp:16-22
+//   - argument checks                xorec_utils.hpp:61-86
+//   - batch recoverability scan      xorec_gpu_cmp.cu:75-81 (require_recovery /
+//                                    is_recoverable, xorec_utils.hpp:144-175)
+//   - stream-ordered H2D bitmap copy xorec_gpu_cmp.cu:83
+// then one kernel launch per call (xec_kernels.hip).
+#include "xec.h"
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstring>
+#include <vector>
+
+#include "xec_kernels.h"
+
+namespace {
+
+std::atomic<bool> g_initialised{false};
+
+// Launch shape (xec_set_launch).  Defaults measured on MI355X, see DESIGN.md.
+std::atomic<int> g_unroll{0};
+std::atomic<int> g_max_grid{0};
+std::atomic<int> g_nt{0};
+
+constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
+constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
+constexpr size_t kAlign = 64;           // XOREC_ALIGNMENT
+
+xec::LaunchShape launch_shape(size_t bs) {
+  xec::LaunchShape ls;
+  int u = g_unroll.load(std::memory_order_relaxed);
+  if (u != 1 && u != 2 && u != 4) {
+    // default: 2 granules per thread once a block holds >= 2 full tiles of 2
+    u = (bs / 16 >= 2u * 2u * xec::kThreads) ? 2 : 1;
+  }
+  ls.unroll = u;
+  ls.max_grid = (uint32_t)g_max_grid.load(std::memory_order_relaxed);
+  ls.nt = g_nt.load(std::memory_order_relaxed) != 0;
+  return ls;
+}
+
+inline uint64_t load_u64(const uint8_t* p) {
+  uint64_t w;
+  std::memcpy(&w, p, 8);
+  return w;
+}
+
+}  // namespace
+
+extern "C" {
+
+xec_status xec_check_args(const void* data, const void* parity, size_t bs, size_t k, size_t m) {
+  if (reinterpret_cast<uintptr_t>(data) % kAlign != 0 ||
+      reinterpret_cast<uintptr_t>(parity) % kAlign != 0)
+    return XEC_INVALID_ALIGNMENT;
+  if (bs < kMinBlock || bs % kBlockMultiple != 0) return XEC_INVALID_SIZE;
+  if (k < 1 || m < 1 || k % m != 0) return XEC_INVALID_COUNTS;
+  return XEC_SUCCESS;
+}
+
+// One pass over the whole S*(k+m)-byte bitmap, 8 bytes at a time.  Only bytes
+// with bit 0 clear are candidates for either rule:
+//   require_recovery: some DATA byte has bit 0 clear (popcount of byte & 1,
+//                     xorec_utils.hpp:144-149);
+//   is_recoverable:   per stripe, per class, at most one ZERO byte among the
+//                     class's data bytes and its parity byte (:160-175).
+// Candidates arrive in increasing position, so the stripe index advances
+// monotonically and the per-class marks are reset lazily per stripe.
+xec_status xec_check_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m, int* needs) {
+  if (needs) *needs = 0;
+  if (k < 1 || m < 1 || k % m != 0) return XEC_INVALID_COUNTS;
+  const size_t row = k + m;
+  const size_t n = S * row;
+  int need = 0;
+  size_t cur_stripe = 0, row_start = 0;
+  std::vector<uint32_t> mark(m, 0);  // stripe+1 that last marked each class
+  auto visit = [&](size_t pos) -> bool {
+    const uint8_t v = bm[pos];
+    if (v & 1u) return true;
+    while (pos >= row_start + row) {
+      row_start += row;
+      ++cur_stripe;
+    }
+    const size_t i = pos - row_start;
+    if (i < k) need = 1;
+    if (v != 0) return true;
+    const size_t cls = i < k ? (m == 1 ? 0 : i % m) : i - k;
+    const uint32_t tag = (uint32_t)cur_stripe + 1u;
+    if (mark[cls] == tag) return false;
+    mark[cls] = tag;
+    return true;
+  };
+  constexpr uint64_t kOnes = 0x0101010101010101ull;
+  size_t pos = 0;
+  for (; pos + 8 <= n; pos += 8) {
+    uint64_t even = ~load_u64(bm + pos) & kOnes;  // bit 0 clear -> low bit of byte set
+    while (even) {
+      int b = __builtin_ctzll(even) >> 3;
+      if (!visit(pos + (size_t)b)) return XEC_DECODE_FAILURE;
+      even &= even - 1;
+    }
+  }
+  for (; pos < n; ++pos)
+    if (!visit(pos)) return XEC_DECODE_FAILURE;
+  if (needs) *needs = need;
+  return XEC_SUCCESS;
+}
+
+xec_status xec_init(int device_id) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return XEC_DEVICE_ERROR;
+  if (device_id < 0 || device_id >= count) return XEC_DEVICE_ERROR;
+  if (hipSetDevice(device_id) != hipSuccess) return XEC_DEVICE_ERROR;
+  g_initialised.store(true, std::memory_order_release);
+  return XEC_SUCCESS;
+}
+
+xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, size_t k, size_t m,
+                      hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
+  if (st != XEC_SUCCESS) return st;
+  if (S == 0) return XEC_SUCCESS;
+  xec::LaunchShape ls = launch_shape(bs);
+  xec::Geometry g = xec::make_geometry(S, bs, k, m, ls.unroll);
+  return xec::launch_encode(d_data, d_parity, g, ls, stream) == hipSuccess ? XEC_SUCCESS
+                                                                           : XEC_DEVICE_ERROR;
+}
+
+xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k, size_t m,
+                      const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
+  if (st != XEC_SUCCESS) return st;
+  if (S == 0) return XEC_SUCCESS;
+  int needs = 0;
+  st = xec_check_bitmap(h_bitmap, S, k, m, &needs);
+  if (st != XEC_SUCCESS) return st;
+  if (!needs) return XEC_SUCCESS;
+  if (hipMemcpyAsync(d_bitmap, h_bitmap, S * (k + m), hipMemcpyHostToDevice, stream) !=
+      hipSuccess)
+    return XEC_DEVICE_ERROR;
+  xec::LaunchShape ls = launch_shape(bs);
+  xec::Geometry g = xec::make_geometry(S, bs, k, m, ls.unroll);
+  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
+             ? XEC_SUCCESS
+             : XEC_DEVICE_ERROR;
+}
+
+xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k, size_t m,
+                     const uint8_t* d_bitmap, hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
+  if (st != XEC_SUCCESS) return st;
+  if (S == 0) return XEC_SUCCESS;
+  xec::Geometry g = xec::make_geometry(S, bs, k, m, 1);
+  return xec::launch_erase(d_data, d_parity, d_bitmap, g, stream) == hipSuccess ? XEC_SUCCESS
+                                                                               : XEC_DEVICE_ERROR;
+}
+
+xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint64_t seed_base,
+                               hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  if (reinterpret_cast<uintptr_t>(d_buf) % 8 != 0) return XEC_INVALID_ALIGNMENT;
+  if (stripe_bytes % 8 != 0) return XEC_INVALID_SIZE;
+  return xec::launch_fill(d_buf, S, stripe_bytes / 8, seed_base, stream) == hipSuccess
+             ? XEC_SUCCESS
+             : XEC_DEVICE_ERROR;
+}
+
+xec_status xec_set_launch(int unroll, int max_grid, int nt) {
+  if (unroll != 0 && unroll != 1 && unroll != 2 && unroll != 4) return XEC_INVALID_SIZE;
+  if (max_grid < 0) return XEC_INVALID_SIZE;
+  g_unroll.store(unroll, std::memory_order_relaxed);
+  g_max_grid.store(max_grid, std::memory_order_relaxed);
+  g_nt.store(nt ? 1 : 0, std::memory_order_relaxed);
+  return XEC_SUCCESS;
+}
+
+const char* xec_status_string(xec_status s) {
+  switch (s) {
+    case XEC_SUCCESS: return "Success";
+    case XEC_INVALID_SIZE: return "InvalidSize";
+    case XEC_INVALID_ALIGNMENT: return "InvalidAlignment";
+    case XEC_INVALID_COUNTS: return "InvalidCounts";
+    case XEC_DECODE_FAILURE: return "DecodeFailure";
+    case XEC_NOT_INITIALIZED: return "NotInitialized";
+    case XEC_DEVICE_ERROR: return "DeviceError";
+  }
+  return "Unknown";
+}
+
+const char* xec_build_info(void) { return "xec-hip gfx950 " __DATE__ " " __TIME__; }
+
+}  // extern "C"

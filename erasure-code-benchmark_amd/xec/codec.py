@@ -1,0 +1,83 @@
+"""Thin Python view of the C ABI (include/xec.h) for tests and bench.py.
+
+Every function forwards to libxec_hip.so and returns the :class:`Status` the
+library returned -- the same 0..4 codes as the reference XorecResult
+(src/xorec/xorec_utils.hpp:26-32).  Device buffers are passed as integer
+addresses or as torch tensors (``.data_ptr()``); streams as a
+``torch.cuda.Stream``, a raw ``hipStream_t`` integer or ``None`` (null stream).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from ._lib import Status, lib
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    if hasattr(x, "ctypes"):  # numpy array (host memory)
+        return int(x.ctypes.data)
+    return int(x)
+
+
+def _stream(s) -> int:
+    if s is None:
+        return 0
+    if hasattr(s, "cuda_stream"):
+        return int(s.cuda_stream)
+    return int(s)
+
+
+def init(device_id: int = 0) -> Status:
+    """xec_init -- replaces xorec_gpu_init + xorec_init (xorec_gpu_cmp.cu:7-27)."""
+    return Status(lib().xec_init(int(device_id)))
+
+
+def encode(d_data, d_parity, S: int, bs: int, k: int, m: int, stream=None) -> Status:
+    """xec_encode -- replaces xorec_gpu_encode (xorec_gpu_cmp.cu:29-55)."""
+    return Status(lib().xec_encode(_ptr(d_data), _ptr(d_parity), S, bs, k, m, _stream(stream)))
+
+
+def decode(d_data, d_parity, S: int, bs: int, k: int, m: int, h_bitmap, d_bitmap,
+           stream=None) -> Status:
+    """xec_decode -- replaces xorec_gpu_decode (xorec_gpu_cmp.cu:57-115); parity read-only."""
+    return Status(lib().xec_decode(_ptr(d_data), _ptr(d_parity), S, bs, k, m, _ptr(h_bitmap),
+                                   _ptr(d_bitmap), _stream(stream)))
+
+
+def erase(d_data, d_parity, S: int, bs: int, k: int, m: int, d_bitmap, stream=None) -> Status:
+    """xec_erase -- device-side simulate_data_loss (abstract_bm.cpp:20-39)."""
+    return Status(lib().xec_erase(_ptr(d_data), _ptr(d_parity), S, bs, k, m, _ptr(d_bitmap),
+                                  _stream(stream)))
+
+
+def fill_splitmix64(d_buf, S: int, stripe_bytes: int, seed_base: int, stream=None) -> Status:
+    return Status(lib().xec_fill_splitmix64(_ptr(d_buf), S, stripe_bytes, seed_base,
+                                            _stream(stream)))
+
+
+def check_bitmap(h_bitmap, S: int, k: int, m: int) -> tuple[Status, bool]:
+    """Host-only recoverability scan; returns (status, needs_recovery)."""
+    needs = ctypes.c_int(0)
+    st = Status(lib().xec_check_bitmap(_ptr(h_bitmap), S, k, m, ctypes.byref(needs)))
+    return st, bool(needs.value)
+
+
+def check_args(data_addr: int, parity_addr: int, bs: int, k: int, m: int) -> Status:
+    """Host-only xorec_check_args (xorec_utils.hpp:61-86)."""
+    return Status(lib().xec_check_args(data_addr, parity_addr, bs, k, m))
+
+
+def set_launch(unroll: int = 0, max_grid: int = 0, nt: int = 0) -> Status:
+    return Status(lib().xec_set_launch(unroll, max_grid, nt))
+
+
+def status_string(st: int) -> str:
+    return lib().xec_status_string(int(st)).decode()
+
+
+def build_info() -> str:
+    return lib().xec_build_info().decode()

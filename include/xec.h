@@ -1,0 +1,121 @@
+/*
+ * xec.h -- C ABI of the MI355X-native XOR-EC hot path (libxec_hip.so).
+ *
+ * This is the drop-in boundary.  It replaces the reference's GPU codec
+ * functions (kenji-k6/erasure-code-benchmark, src/xorec/xorec_gpu_cmp.cuh:14-70)
+ * with plain-C entry points that the reference's codec plugin layer
+ * (src/algorithms/, class AbstractBenchmark, abstract_bm.hpp:18-88) can call
+ * from a new XorecBenchmarkHip plugin; see INTEGRATION.md.
+ *
+ * Batch layout (identical to the reference, abstract_bm.cpp:4-18,
+ * xorec_gpu_cmp.cu:135-144):
+ *   data   : stripe c, data block i   at byte c*k*bs + i*bs
+ *   parity : stripe c, parity block j at byte c*m*bs + j*bs
+ *   bitmap : one byte per block, stripe c at c*(k+m): k data bytes then
+ *            m parity bytes; 0 = lost, nonzero = present.
+ * Parity class of data block i is i % m: parity[j] = XOR of data[i], i%m==j.
+ *
+ * Conventions (reference xorec_gpu_cmp.cu / xorec_gpu_cmp_bm.cpp):
+ *   - the caller owns every buffer, the device bitmap scratch included; the
+ *     codec allocates nothing per call;
+ *   - compute calls are asynchronous on `stream` (NULL = the null stream); the
+ *     caller synchronises (xorec_gpu_cmp_bm.cpp:50,67);
+ *   - status codes 0..4 equal the reference XorecResult
+ *     (xorec_utils.hpp:26-32); 5 and 6 are new; no exception crosses the ABI.
+ *   - use before xec_init returns XEC_NOT_INITIALIZED (the reference throws,
+ *     xorec_gpu_cmp.cu:39,67).
+ */
+#ifndef XEC_H
+#define XEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+typedef enum {
+  XEC_SUCCESS = 0,           /* XorecResult::Success */
+  XEC_INVALID_SIZE = 1,      /* XorecResult::InvalidSize   (bs < 256 or bs % 256) */
+  XEC_INVALID_ALIGNMENT = 2, /* XorecResult::InvalidAlignment (data/parity not 64-B aligned) */
+  XEC_INVALID_COUNTS = 3,    /* XorecResult::InvalidCounts (k < 1, m < 1, k % m) */
+  XEC_DECODE_FAILURE = 4,    /* XorecResult::DecodeFailure (a class lost > 1 block) */
+  XEC_NOT_INITIALIZED = 5,   /* new: xec_init not called / failed */
+  XEC_DEVICE_ERROR = 6       /* new: a HIP runtime call or launch failed */
+} xec_status;
+
+/* Replaces xorec_gpu_init (xorec_gpu_cmp.cuh:14, .cu:7-27) and xorec_init
+ * (xorec.hpp:39, xorec.cpp:16-22).  Selects `device_id` for the calling
+ * thread and marks the library initialised.  Idempotent per device.  Unlike
+ * the reference it takes no k: recovery checks are sized per call, so the
+ * COMPLETE_DATA_BITMAP first-call sizing bug (xorec.cpp:16-22) cannot occur. */
+xec_status xec_init(int device_id);
+
+/* Replaces xorec_gpu_encode (xorec_gpu_cmp.cuh:28-37, .cu:29-55).
+ * parity[c][j] = XOR_{i % m == j} data[c][i] for every stripe c < S.
+ * Arguments are checked exactly like xorec_check_args (xorec_utils.hpp:61-86).
+ * One kernel, no memset, no atomics; parity is fully overwritten.
+ * The reference's num_gpu_blocks/threads_per_block launch arguments are gone:
+ * the launch shape is chosen for gfx950 (see xec_set_launch). */
+xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, size_t k,
+                      size_t m, hipStream_t stream);
+
+/* Replaces xorec_gpu_decode (xorec_gpu_cmp.cuh:57-68, .cu:57-115).
+ * h_bitmap: S*(k+m) bytes of host memory (pinned for an asynchronous copy);
+ * d_bitmap: S*(k+m) bytes of device scratch owned by the caller.
+ * Host checks follow the reference: XEC_DECODE_FAILURE if ANY stripe is
+ * unrecoverable (is_recoverable, xorec_utils.hpp:160-175) and then nothing is
+ * touched; XEC_SUCCESS with no device work if no stripe needs recovery
+ * (require_recovery, xorec_utils.hpp:144-149).  Otherwise h_bitmap is copied
+ * to d_bitmap on `stream` and every lost data block is rebuilt:
+ *   data[c][i] = parity[c][i%m] ^ XOR_{l%m == i%m, l != i} data[c][l].
+ * Lost parity is not regenerated.  Parity is READ-ONLY here, as in the CPU
+ * decode (xorec.cpp:62-111) -- deliberately unlike the reference GPU decode,
+ * which folds all data into parity (xorec_gpu_cmp.cu:94-102).  The content of
+ * lost data blocks on entry is irrelevant (no zeroing pre-condition). */
+xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
+                      size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream);
+
+/* Host-only recoverability scan used by xec_decode (no GPU needed):
+ * returns XEC_DECODE_FAILURE if some stripe is unrecoverable, else
+ * XEC_SUCCESS and sets *needs_recovery to 1 iff some stripe needs recovery. */
+xec_status xec_check_bitmap(const uint8_t* h_bitmap, size_t S, size_t k, size_t m,
+                            int* needs_recovery);
+
+/* Host-only argument check, identical to xorec_check_args
+ * (xorec_utils.hpp:61-86); pointers are only tested for 64-B alignment. */
+xec_status xec_check_args(const void* data, const void* parity, size_t bs, size_t k, size_t m);
+
+/* Device-side erasure injection (the GPU analogue of
+ * AbstractBenchmark::simulate_data_loss, abstract_bm.cpp:20-39, without the
+ * per-block host memsets of xorec_gpu_cmp_bm.cpp:71-89): zero every block
+ * whose d_bitmap byte is 0, data and parity alike. */
+xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k, size_t m,
+                     const uint8_t* d_bitmap, hipStream_t stream);
+
+/* Synthetic input generator (tests and bench): stripe c's stripe_bytes are
+ * little-endian u64 splitmix64 outputs from state seed_base + c.
+ * stripe_bytes % 8 == 0 and d_buf 8-B aligned, else XEC_INVALID_SIZE /
+ * XEC_INVALID_ALIGNMENT. */
+xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint64_t seed_base,
+                               hipStream_t stream);
+
+/* Launch-shape override for tuning sweeps: granules (16 B) per thread per
+ * member `unroll` (1, 2 or 4), `max_grid` workgroups (0 = one per tile),
+ * `nt` = 1 for non-temporal loads and stores.  Pass zeros to restore the
+ * defaults.  Process-wide; not thread-safe against concurrent launches. */
+xec_status xec_set_launch(int unroll, int max_grid, int nt);
+
+/* Human-readable status name ("Success", "InvalidSize", ...). */
+const char* xec_status_string(xec_status s);
+
+/* Build identification, e.g. "xec-hip gfx950 <date>". */
+const char* xec_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XEC_H */

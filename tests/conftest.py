@@ -1,0 +1,50 @@
+"""Shared pytest setup.
+
+* ``-m gpu`` tests need a real MI355X (run through gpurun); everything else runs
+  on the CPU-only container.
+* The oracle (oracle/xorec_oracle.py) is imported only here and in tests, as the
+  checker -- never as the thing under test.
+"""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG_DIR = ROOT / "erasure-code-benchmark_amd"
+for p in (ROOT, PKG_DIR, ROOT / "oracle"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+@pytest.fixture(scope="session")
+def known_answers() -> dict:
+    return json.loads((GOLDEN / "known_answers.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import xorec_oracle as xo
+    return xo.COracle()
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """Initialised xec on cuda:0 (HIP path); fails loudly if the library is missing."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no GPU is visible")
+    import xec
+    st = xec.init(0)
+    assert st == xec.Status.SUCCESS, f"xec_init failed: {st!r}"
+    torch.cuda.set_device(0)
+    return xec

@@ -1,0 +1,135 @@
+"""The C ABI library loads, exports include/xec.h, and its host-only logic
+matches the oracle (CPU only: no compute call needs a GPU here)."""
+from __future__ import annotations
+
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import xorec_oracle as xo
+import xec
+from conftest import ROOT
+
+
+def header_symbols() -> set[str]:
+    text = (ROOT / "include" / "xec.h").read_text()
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(xec_\w+)\s*\(", text, re.M))
+
+
+def test_header_and_binding_agree():
+    assert header_symbols() == set(xec.EXPORTED)
+
+
+def test_library_exports_every_header_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", str(xec.LIB_PATH)], check=True,
+                         capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = header_symbols() - exported
+    assert not missing, f"libxec_hip.so lacks {missing}"
+    L = xec.lib()
+    for name in header_symbols():
+        assert getattr(L, name) is not None
+
+
+def test_library_is_hip_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading",
+                          str(xec.LIB_PATH)], capture_output=True, text=True)
+    assert "gfx950" in out.stdout + out.stderr or b"gfx950" in xec.LIB_PATH.read_bytes()
+    assert "gfx950" in xec.build_info()
+
+
+def test_status_strings():
+    names = ["Success", "InvalidSize", "InvalidAlignment", "InvalidCounts", "DecodeFailure",
+             "NotInitialized", "DeviceError"]
+    for code, name in enumerate(names):
+        assert xec.status_string(code) == name
+        assert xec.Status(code).value == code
+
+
+def test_compute_before_init_is_not_initialized():
+    # xec_init never succeeded in a GPU-less process, so every compute entry
+    # point must refuse before touching the device (reference throws instead).
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present; covered by the process-level GPU tests")
+    assert xec.init(0) == xec.Status.DEVICE_ERROR
+    S, k, m, bs = 1, 4, 1, 4096
+    assert xec.encode(64, 128, S, bs, k, m) == xec.Status.NOT_INITIALIZED
+    bm = np.ones(5, dtype=np.uint8)
+    assert xec.decode(64, 128, S, bs, k, m, bm, 256) == xec.Status.NOT_INITIALIZED
+    assert xec.erase(64, 128, S, bs, k, m, 256) == xec.Status.NOT_INITIALIZED
+    assert xec.fill_splitmix64(64, S, 4096, 1) == xec.Status.NOT_INITIALIZED
+
+
+def test_check_args_matches_golden(known_answers):
+    for e in known_answers["status"]:
+        st = xec.check_args(4096 + e["data_misalign"], 8192 + e["parity_misalign"], e["bs"], e["k"],
+                            e["m"])
+        assert st == e["encode"], e
+
+
+@pytest.mark.parametrize("bs", [0, 1, 64, 100, 255, 256, 257, 320, 512, 768, 4096, 4352,
+                                1 << 20, (1 << 20) + 128])
+@pytest.mark.parametrize("k,m", [(0, 1), (1, 0), (4, 1), (6, 4), (8, 4), (1, 1), (3, 2)])
+def test_check_args_matches_oracle(oracle, bs, k, m):
+    for da, pa in [(0, 0), (64, 0), (0, 64), (8, 0), (0, 16), (32, 48)]:
+        want = oracle.check_args(4096 + da, 8192 + pa, bs, k, m)
+        assert xec.check_args(4096 + da, 8192 + pa, bs, k, m) == want
+
+
+def _oracle_batch_check(k, m, rows):
+    need = False
+    for r in rows:
+        if xo.np_require_recovery(k, r):
+            need = True
+        if not xo.np_is_recoverable(k, m, r):
+            return xo.DECODE_FAILURE, False
+    return xo.SUCCESS, need
+
+
+def test_check_bitmap_random(oracle):
+    rng = np.random.default_rng(1896)
+    for trial in range(1500):
+        m = int(rng.choice([1, 2, 3, 4, 8]))
+        k = m * int(rng.integers(1, 9))
+        S = int(rng.integers(1, 40))
+        p_loss = float(rng.choice([0.0, 0.02, 0.1, 0.3]))
+        bm = (rng.random((S, k + m)) >= p_loss).astype(np.uint8)
+        if trial % 5 == 0:  # values with bit 0 clear but nonzero, and odd values > 1
+            bm[rng.random((S, k + m)) < 0.05] = rng.choice([2, 3, 4, 255])
+        want = _oracle_batch_check(k, m, bm)
+        got_st, got_need = xec.check_bitmap(bm.reshape(-1), S, k, m)
+        assert int(got_st) == want[0], (k, m, S, bm)
+        if want[0] == xo.SUCCESS:
+            assert got_need == want[1], (k, m, S, bm)
+
+
+def test_check_bitmap_golden_patterns(known_answers):
+    from conftest import GOLDEN
+    for e in known_answers["decode"]:
+        k, m, S = e["k"], e["m"], e["S"]
+        bm = np.fromfile(GOLDEN / "patterns" / e["pattern"], dtype=np.uint8)
+        st, need = xec.check_bitmap(bm, S, k, m)
+        assert (st == xec.Status.DECODE_FAILURE) == ("4" in e["codes"]), e
+        if st == xec.Status.SUCCESS:
+            assert need == any(xo.np_require_recovery(k, bm[c * (k + m):(c + 1) * (k + m)])
+                               for c in range(S))
+
+
+def test_check_bitmap_single_erasure_large():
+    S, k, m = 65536, 32, 1
+    bm = xo.single_erasure_bitmap(S, k, m)
+    st, need = xec.check_bitmap(bm, S, k, m)
+    assert st == xec.Status.SUCCESS and need
+    bm2 = bm.copy()
+    bm2[(S - 1) * (k + m) + k] = 0  # last stripe also loses its parity -> unrecoverable
+    assert xec.check_bitmap(bm2, S, k, m)[0] == xec.Status.DECODE_FAILURE
+    assert xec.check_bitmap(np.ones(S * (k + m), np.uint8), S, k, m) == (xec.Status.SUCCESS, False)
+
+
+def test_set_launch_validation():
+    assert xec.set_launch(3, 0, 0) == xec.Status.INVALID_SIZE
+    assert xec.set_launch(1, -1, 0) == xec.Status.INVALID_SIZE
+    assert xec.set_launch(0, 0, 0) == xec.Status.SUCCESS

@@ -1,0 +1,189 @@
+"""Parity of the HIP path (libxec_hip.so on an MI355X) against the CPU oracle.
+
+Bit-exact: parity after encode, every data block after erase+decode, parity
+untouched by decode.  Sizes: every golden fixture shape (checked against the
+reference-generated hashes too), the BASELINE.json configs at full size, and
+edge shapes (S = 0/1, minimum block, ragged tiles, generic member counts).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import xorec_oracle as xo
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+SEED = xo.RANDOM_SEED
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class Batch:
+    """Device batch filled on the GPU with the shared splitmix64 convention."""
+
+    def __init__(self, xec, S, k, m, bs, seed=SEED, pad=0):
+        torch = _torch()
+        self.S, self.k, self.m, self.bs = S, k, m, bs
+        self.stream = torch.cuda.current_stream()
+        self.d = torch.empty(max(S * k * bs, 1) + pad, dtype=torch.uint8, device="cuda")
+        self.p = torch.full((max(S * m * bs, 1) + pad,), 0xEE, dtype=torch.uint8, device="cuda")
+        if S:
+            assert xec.fill_splitmix64(self.d, S, k * bs, seed, self.stream) == xec.Status.SUCCESS
+
+    def data(self) -> np.ndarray:
+        _torch().cuda.synchronize()
+        return self.d[: self.S * self.k * self.bs].cpu().numpy()
+
+    def parity(self) -> np.ndarray:
+        _torch().cuda.synchronize()
+        return self.p[: self.S * self.m * self.bs].cpu().numpy()
+
+
+def encode_and_check(xec, oracle, S, k, m, bs, seed=SEED):
+    b = Batch(xec, S, k, m, bs, seed)
+    assert xec.encode(b.d, b.p, S, bs, k, m, b.stream) == xec.Status.SUCCESS
+    ref_d, ref_p = oracle.batch(S, k, m, bs, seed_base=seed)
+    assert np.array_equal(b.data(), ref_d), "device fill differs from oracle fill"
+    assert np.array_equal(b.parity(), ref_p), f"parity mismatch {(S, k, m, bs)}"
+    return b, ref_d, ref_p
+
+
+def erase_decode_check(xec, b, ref_d, ref_p, bm, expect=0):
+    torch = _torch()
+    S, k, m, bs = b.S, b.k, b.m, b.bs
+    h_bm = torch.from_numpy(np.ascontiguousarray(bm)).pin_memory()
+    d_bm = h_bm.to("cuda")
+    assert xec.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == xec.Status.SUCCESS
+    erased_d, erased_p = b.data(), b.parity()
+    scratch = torch.empty_like(d_bm)
+    st = xec.decode(b.d, b.p, S, bs, k, m, h_bm, scratch, b.stream)
+    assert st == expect
+    got_d, got_p = b.data(), b.parity()
+    assert np.array_equal(got_p, erased_p), "decode wrote parity"
+    if expect == xec.Status.SUCCESS:
+        assert np.array_equal(got_d, ref_d), "recovered data mismatch"
+    else:
+        assert np.array_equal(got_d, erased_d), "failed decode modified data"
+    # the erased parity is exactly the oracle parity with lost parity blocks zeroed
+    rows = bm.reshape(S, k + m)
+    want_p = ref_p.reshape(S, m, bs).copy()
+    want_p[rows[:, k:] == 0] = 0
+    assert np.array_equal(erased_p.reshape(S, m, bs), want_p)
+
+
+# --------------------------------------------------------------------------
+def test_golden_encode_fixtures(gpu, oracle, known_answers):
+    """Every reference-generated known answer, through the HIP path."""
+    for e in known_answers["encode"]:
+        b = Batch(gpu, e["S"], e["k"], e["m"], e["bs"], known_answers["seed"])
+        assert gpu.encode(b.d, b.p, e["S"], e["bs"], e["k"], e["m"], b.stream) == 0
+        assert f"{oracle.fnv1a64(b.parity()):016x}" == e["parity_fnv"], e
+
+
+def test_golden_cfg1_raw(gpu):
+    b = Batch(gpu, 1, 4, 1, 4096)
+    assert gpu.encode(b.d, b.p, 1, 4096, 4, 1, b.stream) == 0
+    ref = np.fromfile(GOLDEN / "cfg1_parity_k4_m1_4096.bin", dtype=np.uint8)
+    assert np.array_equal(b.parity(), ref)
+
+
+def test_golden_decode_fixtures(gpu, oracle, known_answers):
+    for e in known_answers["decode"]:
+        k, m, bs, S = e["k"], e["m"], e["bs"], e["S"]
+        bm = np.fromfile(GOLDEN / "patterns" / e["pattern"], dtype=np.uint8)
+        b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs, known_answers["seed"])
+        expect = gpu.Status.DECODE_FAILURE if "4" in e["codes"] else gpu.Status.SUCCESS
+        erase_decode_check(gpu, b, ref_d, ref_p, bm, expect)
+        if expect == gpu.Status.SUCCESS:
+            assert f"{oracle.fnv1a64(b.data()):016x}" == e["data_fnv_after"]
+            assert f"{oracle.fnv1a64(b.parity()):016x}" == e["parity_fnv_after"]
+
+
+@pytest.mark.parametrize("S,k,m,bs", [
+    (1, 4, 1, 4096),          # BASELINE config 1 shape
+    (1024, 8, 1, 65536),      # config 2 (full size)
+    (256, 16, 1, 1 << 20),    # config 3 (full size: 4 GiB data)
+    (65536, 32, 1, 4096),     # config 4 (full size: 8 GiB data, > 4 GiB offsets)
+])
+def test_baseline_configs_full_size(gpu, oracle, S, k, m, bs):
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    erase_decode_check(gpu, b, ref_d, ref_p, xo.single_erasure_bitmap(S, k, m))
+
+
+@pytest.mark.parametrize("S,k,m,bs", [
+    (1, 1, 1, 256), (3, 2, 2, 512), (2, 5, 1, 768), (3, 40, 8, 4352), (2, 64, 1, 256),
+    (5, 6, 3, 512), (7, 12, 4, 2048), (9, 24, 8, 1024), (4, 36, 4, 4096), (3, 40, 8, 8192),
+    (33, 16, 1, 8448), (17, 3, 1, 256 * 129), (5, 128, 2, 1024),
+])
+def test_edge_shapes_multi_erasure(gpu, oracle, S, k, m, bs):
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    bm = np.ones((S, k + m), dtype=np.uint8)
+    for c in range(S):
+        oracle.select_lost_blocks(k, m, 1 + c % m, bm[c], c)
+    erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+
+
+def test_empty_batch_is_noop(gpu):
+    torch = _torch()
+    d = torch.empty(64, dtype=torch.uint8, device="cuda")
+    assert gpu.encode(d, d, 0, 4096, 4, 1) == gpu.Status.SUCCESS
+    assert gpu.decode(d, d, 0, 4096, 4, 1, np.zeros(1, np.uint8), d) == gpu.Status.SUCCESS
+
+
+def test_no_loss_and_parity_only_loss_touch_nothing(gpu, oracle):
+    S, k, m, bs = 8, 8, 4, 1024
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    erase_decode_check(gpu, b, ref_d, ref_p, np.ones(S * (k + m), np.uint8))
+    bm = np.ones((S, k + m), np.uint8)
+    bm[:, k:] = 0
+    erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+
+
+def test_argument_errors_launch_nothing(gpu):
+    torch = _torch()
+    d = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    p = torch.zeros(1 << 14, dtype=torch.uint8, device="cuda")
+    S = gpu.Status
+    assert gpu.encode(d.data_ptr() + 16, p, 1, 4096, 4, 1) == S.INVALID_ALIGNMENT
+    assert gpu.encode(d, p.data_ptr() + 32, 1, 4096, 4, 1) == S.INVALID_ALIGNMENT
+    assert gpu.encode(d, p, 1, 100, 4, 1) == S.INVALID_SIZE
+    assert gpu.encode(d, p, 1, 4096, 6, 4) == S.INVALID_COUNTS
+    assert gpu.encode(d, p, 1, 4096, 0, 1) == S.INVALID_COUNTS
+    bm = np.ones(5, np.uint8)
+    assert gpu.decode(d, p, 1, 320, 4, 1, bm, p) == S.INVALID_SIZE
+    torch.cuda.synchronize()
+    assert int(p.sum()) == 0
+
+
+@pytest.mark.parametrize("unroll", [1, 2, 4])
+@pytest.mark.parametrize("max_grid,nt", [(0, 0), (0, 1), (300, 0), (2048, 1)])
+def test_launch_shapes_bit_exact(gpu, oracle, unroll, max_grid, nt):
+    assert gpu.set_launch(unroll, max_grid, nt) == gpu.Status.SUCCESS
+    try:
+        for (S, k, m, bs) in [(24, 16, 1, 65536), (40, 32, 4, 4352), (9, 10, 2, 2816)]:
+            b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+            bm = np.ones((S, k + m), np.uint8)
+            for c in range(S):
+                oracle.select_lost_blocks(k, m, m, bm[c], 77 + c)
+            erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+    finally:
+        gpu.set_launch(0, 0, 0)
+
+
+def test_encode_is_linear(gpu):
+    """Size-independent property at a full config shape: E(a ^ b) == E(a) ^ E(b)."""
+    torch = _torch()
+    S, k, m, bs = 256, 16, 1, 1 << 20
+    a = Batch(gpu, S, k, m, bs, seed=11)
+    bb = Batch(gpu, S, k, m, bs, seed=22)
+    ab = torch.bitwise_xor(a.d, bb.d)
+    pab = torch.empty_like(a.p)
+    for x, px in ((a.d, a.p), (bb.d, bb.p), (ab, pab)):
+        assert gpu.encode(x, px, S, bs, k, m, a.stream) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(torch.bitwise_xor(a.p, bb.p), pab)
