@@ -79,12 +79,12 @@ def cpu_baseline(k, m, bs, budget_s):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     threads = min(threads, os.cpu_count() or threads)
     o = xo.COracle()
-    S = 32  # 32 stripes x 16 x 1 MiB = 512 MiB data, 2x a typical host LLC+
+    S = 64  # 64 stripes x 16 x 1 MiB = 1 GiB data: beyond any host LLC
     data, parity = o.batch(S, k, m, bs, threads=threads)
     bm = xo.single_erasure_bitmap(S, k, m)
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
     reps, t_tot = 0, 0.0
-    while t_tot < budget_s and reps < 200:
+    while t_tot < budget_s and reps < 2000:
         t0 = time.perf_counter()
         assert o.encode_batch(data, parity, S, bs, k, m, threads) == 0
         assert o.decode_batch(data, parity, S, bs, k, m, bm, threads) == 0

@@ -21,7 +21,7 @@ namespace {
 
 std::atomic<bool> g_initialised{false};
 
-// Launch shape (xec_set_launch).  Defaults measured on MI355X, see DESIGN.md.
+// Launch-shape overrides (xec_set_launch); 0 = default.
 std::atomic<int> g_unroll{0};
 std::atomic<int> g_max_grid{0};
 std::atomic<int> g_nt{0};
@@ -30,16 +30,18 @@ constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
 constexpr size_t kAlign = 64;           // XOREC_ALIGNMENT
 
-xec::LaunchShape launch_shape(size_t bs) {
+// Defaults measured on MI355X (tools/sweep.py, profiles/sweep_*.json):
+// non-temporal loads and stores win for both kernels (every byte is touched
+// once); encode prefers one workgroup per 4 KiB tile, decode amortises its
+// bitmap lookup over 8 KiB tiles in a 4096-workgroup grid-stride launch.
+xec::LaunchShape launch_shape(size_t bs, bool decode) {
   xec::LaunchShape ls;
   int u = g_unroll.load(std::memory_order_relaxed);
-  if (u != 1 && u != 2 && u != 4) {
-    // default: 2 granules per thread once a block holds >= 2 full tiles of 2
-    u = (bs / 16 >= 2u * 2u * xec::kThreads) ? 2 : 1;
-  }
+  if (u != 1 && u != 2 && u != 4) u = (decode && bs / 16 >= 2u * xec::kThreads) ? 2 : 1;
   ls.unroll = u;
-  ls.max_grid = (uint32_t)g_max_grid.load(std::memory_order_relaxed);
-  ls.nt = g_nt.load(std::memory_order_relaxed) != 0;
+  int g = g_max_grid.load(std::memory_order_relaxed);
+  ls.max_grid = g > 0 ? (uint32_t)g : (decode ? 4096u : 0u);
+  ls.nt = g_nt.load(std::memory_order_relaxed) != 2;
   return ls;
 }
 
@@ -125,7 +127,7 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
-  xec::LaunchShape ls = launch_shape(bs);
+  xec::LaunchShape ls = launch_shape(bs, false);
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls.unroll);
   return xec::launch_encode(d_data, d_parity, g, ls, stream) == hipSuccess ? XEC_SUCCESS
                                                                            : XEC_DEVICE_ERROR;
@@ -144,7 +146,7 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   if (hipMemcpyAsync(d_bitmap, h_bitmap, S * (k + m), hipMemcpyHostToDevice, stream) !=
       hipSuccess)
     return XEC_DEVICE_ERROR;
-  xec::LaunchShape ls = launch_shape(bs);
+  xec::LaunchShape ls = launch_shape(bs, true);
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls.unroll);
   return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
              ? XEC_SUCCESS
@@ -172,12 +174,12 @@ xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint6
              : XEC_DEVICE_ERROR;
 }
 
-xec_status xec_set_launch(int unroll, int max_grid, int nt) {
+xec_status xec_set_launch(int unroll, int max_grid, int cache_policy) {
   if (unroll != 0 && unroll != 1 && unroll != 2 && unroll != 4) return XEC_INVALID_SIZE;
-  if (max_grid < 0) return XEC_INVALID_SIZE;
+  if (max_grid < 0 || cache_policy < 0 || cache_policy > 2) return XEC_INVALID_SIZE;
   g_unroll.store(unroll, std::memory_order_relaxed);
   g_max_grid.store(max_grid, std::memory_order_relaxed);
-  g_nt.store(nt ? 1 : 0, std::memory_order_relaxed);
+  g_nt.store(cache_policy, std::memory_order_relaxed);
   return XEC_SUCCESS;
 }
 

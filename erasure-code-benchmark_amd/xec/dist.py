@@ -1,0 +1,84 @@
+"""Multi-GPU plumbing for stripe-partitioned XOR-EC.
+
+One process per GPU.  Stripes are independent, so the codec itself needs no
+collective: each rank encodes / decodes the contiguous stripe range
+:func:`xec.partition.stripe_range` assigns it.  The only exchanges are
+
+* ``scatter_stripes`` -- the root hands each rank its slice of a batch that
+  starts on the root (the reference's single-GPU batch, xorec_gpu_cmp_bm.cpp:
+  25-37, spread over the node); point-to-point send/recv because ranges are
+  ragged and RCCL has no scatter primitive; over xGMI with backend "nccl"
+  (RCCL), over TCP with "gloo" (CPU tests);
+* ``gather_stripes`` -- the inverse, e.g. parity or recovered blocks back to
+  the root;
+* ``max_over_ranks`` -- the timing reduction of bench.py.
+
+The root's egress is bounded by its xGMI links, far below HBM bandwidth, so
+scatter-inclusive rates are reported separately from the device-resident
+metric.
+"""
+from __future__ import annotations
+
+from .partition import stripe_range
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist
+
+
+def scatter_stripes(full, local, S_total: int, stripe_bytes: int, root: int = 0):
+    """Copy stripes [start, stop) of ``full`` (uint8, S_total*stripe_bytes, only
+    read on ``root``) into ``local`` (uint8, (stop-start)*stripe_bytes) on every
+    rank.  Returns ``local``."""
+    dist = _dist()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if rank == root:
+        ops = []
+        for r in range(world):
+            a, b = stripe_range(S_total, r, world)
+            piece = full[a * stripe_bytes:b * stripe_bytes]
+            if r == root:
+                local.copy_(piece)
+            elif b > a:
+                ops.append(dist.P2POp(dist.isend, piece, r))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+    else:
+        a, b = stripe_range(S_total, rank, world)
+        if b > a:
+            dist.recv(local, src=root)
+    return local
+
+
+def gather_stripes(local, full, S_total: int, stripe_bytes: int, root: int = 0):
+    """Inverse of :func:`scatter_stripes`: every rank's ``local`` slice lands in
+    ``full`` on ``root`` (``full`` is ignored elsewhere)."""
+    dist = _dist()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if rank == root:
+        ops = []
+        for r in range(world):
+            a, b = stripe_range(S_total, r, world)
+            piece = full[a * stripe_bytes:b * stripe_bytes]
+            if r == root:
+                piece.copy_(local)
+            elif b > a:
+                ops.append(dist.P2POp(dist.irecv, piece, r))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+    else:
+        a, b = stripe_range(S_total, rank, world)
+        if b > a:
+            dist.send(local, dst=root)
+    return full
+
+
+def max_over_ranks(values, device=None):
+    """Element-wise max of a list of floats over all ranks (bench timing)."""
+    import torch
+    dist = _dist()
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()

@@ -103,11 +103,12 @@ xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k
 xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint64_t seed_base,
                                hipStream_t stream);
 
-/* Launch-shape override for tuning sweeps: granules (16 B) per thread per
- * member `unroll` (1, 2 or 4), `max_grid` workgroups (0 = one per tile),
- * `nt` = 1 for non-temporal loads and stores.  Pass zeros to restore the
- * defaults.  Process-wide; not thread-safe against concurrent launches. */
-xec_status xec_set_launch(int unroll, int max_grid, int nt);
+/* Launch-shape override for tuning sweeps (process-wide, not thread-safe
+ * against concurrent launches).  Each argument 0 = the measured default:
+ *   unroll       16-byte granules per thread per class member: 1, 2 or 4;
+ *   max_grid     workgroups per launch (grid-stride beyond), 0 = one per tile;
+ *   cache_policy 1 = non-temporal loads/stores (nt), 2 = default policy. */
+xec_status xec_set_launch(int unroll, int max_grid, int cache_policy);
 
 /* Human-readable status name ("Success", "InvalidSize", ...). */
 const char* xec_status_string(xec_status s);

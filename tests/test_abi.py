@@ -132,4 +132,5 @@ def test_check_bitmap_single_erasure_large():
 def test_set_launch_validation():
     assert xec.set_launch(3, 0, 0) == xec.Status.INVALID_SIZE
     assert xec.set_launch(1, -1, 0) == xec.Status.INVALID_SIZE
+    assert xec.set_launch(1, 0, 3) == xec.Status.INVALID_SIZE
     assert xec.set_launch(0, 0, 0) == xec.Status.SUCCESS

@@ -161,7 +161,7 @@ def test_argument_errors_launch_nothing(gpu):
 
 
 @pytest.mark.parametrize("unroll", [1, 2, 4])
-@pytest.mark.parametrize("max_grid,nt", [(0, 0), (0, 1), (300, 0), (2048, 1)])
+@pytest.mark.parametrize("max_grid,nt", [(0, 2), (0, 1), (300, 2), (2048, 1), (0, 0)])
 def test_launch_shapes_bit_exact(gpu, oracle, unroll, max_grid, nt):
     assert gpu.set_launch(unroll, max_grid, nt) == gpu.Status.SUCCESS
     try:

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Profile bench.py on the GPU box: kernel trace + stats, then one PMC pass per
+# counter group (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950).
+# Usage (inside gpurun): bash tools/gpu_profile.sh <tag> [bench args...]
+set -euo pipefail
+TAG=${1:?tag}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$R"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o kt --output-format csv \
+  -- python3 bench.py --no-cpu-baseline "$@" > "$OUT/bench_trace.log" 2>&1
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -d "$OUT/pmc_$C" -o pmc --output-format csv \
+    -- python3 bench.py --no-cpu-baseline --no-verify --steps 5 --warmup 2 "$@" > "$OUT/bench_$C.log" 2>&1
+done
+echo "profile $TAG done"

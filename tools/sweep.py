@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--unroll", default="1,2,4")
     ap.add_argument("--grid", default="0,2048,4096")
-    ap.add_argument("--nt", default="0,1")
+    ap.add_argument("--nt", default="1,2", help="cache policy: 1 nt, 2 default")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
