@@ -1,0 +1,166 @@
+// xec_pipeline.cpp -- host-in / host-out XOR-EC.
+//
+// The MI355X analogue of the reference's GPU-memory / unified-memory
+// variants (src/algorithms/xorec_gpu_ptr_bm.cpp:17-65,
+// xorec_unified_ptr_bm.cpp:15-86), which move data between host and device
+// and compute on the CPU.  Here the data starts and ends in (pinned) host
+// memory and the codec runs on the GPU: the batch is cut into chunks of
+// `chunk_stripes` stripes and each chunk goes
+//     H2D (data [+ parity])  ->  kernel  ->  D2H (parity | recovered blocks)
+// on one of `nstreams` streams with its own device slot, so chunk i's copies
+// overlap chunk i±1's copies and kernels.  PCIe, not HBM, bounds this path.
+#include <hip/hip_runtime.h>
+
+#include <new>
+#include <vector>
+
+#include "xec.h"
+#include "xec_kernels.h"
+
+struct xec_pipeline {
+  int device = 0;
+  size_t chunk_stripes = 0, bs = 0, k = 0, m = 0;
+  struct Slot {
+    hipStream_t stream = nullptr;
+    uint8_t* data = nullptr;
+    uint8_t* parity = nullptr;
+    uint8_t* bitmap = nullptr;
+  };
+  std::vector<Slot> slots;
+};
+
+namespace {
+
+void destroy_slots(xec_pipeline* p) {
+  for (auto& s : p->slots) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    (void)hipFree(s.data);
+    (void)hipFree(s.parity);
+    (void)hipFree(s.bitmap);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  p->slots.clear();
+}
+
+xec_status sync_all(xec_pipeline* p) {
+  xec_status st = XEC_SUCCESS;
+  for (auto& s : p->slots)
+    if (hipStreamSynchronize(s.stream) != hipSuccess) st = XEC_DEVICE_ERROR;
+  return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+xec_status xec_pipeline_create(xec_pipeline** out, size_t chunk_stripes, size_t bs, size_t k,
+                               size_t m, int nstreams) {
+  if (!out) return XEC_INVALID_SIZE;
+  *out = nullptr;
+  // the pipeline's device slots are 64-B aligned by hipMalloc; check the rest
+  xec_status st = xec_check_args(reinterpret_cast<void*>(64), reinterpret_cast<void*>(64), bs, k, m);
+  if (st != XEC_SUCCESS) return st;
+  if (chunk_stripes == 0 || nstreams < 1 || nstreams > 16) return XEC_INVALID_SIZE;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
+  auto* p = new (std::nothrow) xec_pipeline;
+  if (!p) return XEC_DEVICE_ERROR;
+  p->device = dev;
+  p->chunk_stripes = chunk_stripes;
+  p->bs = bs;
+  p->k = k;
+  p->m = m;
+  p->slots.resize(static_cast<size_t>(nstreams));
+  for (auto& s : p->slots) {
+    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&s.data, chunk_stripes * k * bs) != hipSuccess ||
+        hipMalloc(&s.parity, chunk_stripes * m * bs) != hipSuccess ||
+        hipMalloc(&s.bitmap, chunk_stripes * (k + m)) != hipSuccess) {
+      destroy_slots(p);
+      delete p;
+      return XEC_DEVICE_ERROR;
+    }
+  }
+  *out = p;
+  return XEC_SUCCESS;
+}
+
+xec_status xec_pipeline_destroy(xec_pipeline* p) {
+  if (!p) return XEC_SUCCESS;
+  destroy_slots(p);
+  delete p;
+  return XEC_SUCCESS;
+}
+
+xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_parity, size_t S) {
+  if (!p) return XEC_NOT_INITIALIZED;
+  const size_t k = p->k, m = p->m, bs = p->bs;
+  const auto* src = static_cast<const uint8_t*>(h_data);
+  auto* dst = static_cast<uint8_t*>(h_parity);
+  size_t chunk = 0;
+  for (size_t c0 = 0; c0 < S; c0 += p->chunk_stripes, ++chunk) {
+    auto& s = p->slots[chunk % p->slots.size()];
+    const size_t n = (S - c0) < p->chunk_stripes ? (S - c0) : p->chunk_stripes;
+    // stream order serialises reuse of this slot behind its previous chunk
+    if (hipMemcpyAsync(s.data, src + c0 * k * bs, n * k * bs, hipMemcpyHostToDevice, s.stream) !=
+        hipSuccess)
+      return XEC_DEVICE_ERROR;
+    xec_status st = xec_encode(s.data, s.parity, n, bs, k, m, s.stream);
+    if (st != XEC_SUCCESS) return st;
+    if (hipMemcpyAsync(dst + c0 * m * bs, s.parity, n * m * bs, hipMemcpyDeviceToHost, s.stream) !=
+        hipSuccess)
+      return XEC_DEVICE_ERROR;
+  }
+  return sync_all(p);
+}
+
+xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_parity, size_t S,
+                               const uint8_t* h_bitmap) {
+  if (!p) return XEC_NOT_INITIALIZED;
+  const size_t k = p->k, m = p->m, bs = p->bs, row = k + m;
+  int needs = 0;
+  xec_status st = xec_check_bitmap(h_bitmap, S, k, m, &needs);
+  if (st != XEC_SUCCESS || !needs) return st;  // all-or-nothing, as xec_decode
+  auto* data = static_cast<uint8_t*>(h_data);
+  const auto* par = static_cast<const uint8_t*>(h_parity);
+  size_t chunk = 0;
+  for (size_t c0 = 0; c0 < S; c0 += p->chunk_stripes, ++chunk) {
+    auto& s = p->slots[chunk % p->slots.size()];
+    const size_t n = (S - c0) < p->chunk_stripes ? (S - c0) : p->chunk_stripes;
+    bool any_lost = false;
+    for (size_t c = c0; c < c0 + n && !any_lost; ++c)
+      for (size_t i = 0; i < k; ++i)
+        if (h_bitmap[c * row + i] == 0) {
+          any_lost = true;
+          break;
+        }
+    if (!any_lost) continue;  // nothing of this chunk crosses the link
+    if (hipMemcpyAsync(s.data, data + c0 * k * bs, n * k * bs, hipMemcpyHostToDevice, s.stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(s.parity, par + c0 * m * bs, n * m * bs, hipMemcpyHostToDevice, s.stream) !=
+            hipSuccess)
+      return XEC_DEVICE_ERROR;
+    st = xec_decode(s.data, s.parity, n, bs, k, m, h_bitmap + c0 * row, s.bitmap, s.stream);
+    if (st != XEC_SUCCESS) return st;
+    // only the rebuilt blocks go back; adjacent lost blocks merge into one copy
+    for (size_t c = c0; c < c0 + n; ++c) {
+      size_t i = 0;
+      while (i < k) {
+        if (h_bitmap[c * row + i] != 0) {
+          ++i;
+          continue;
+        }
+        size_t j = i;
+        while (j < k && h_bitmap[c * row + j] == 0) ++j;
+        const size_t off = (c - c0) * k * bs + i * bs;
+        if (hipMemcpyAsync(data + c * k * bs + i * bs, s.data + off, (j - i) * bs,
+                           hipMemcpyDeviceToHost, s.stream) != hipSuccess)
+          return XEC_DEVICE_ERROR;
+        i = j;
+      }
+    }
+  }
+  return sync_all(p);
+}
+
+}  // extern "C"

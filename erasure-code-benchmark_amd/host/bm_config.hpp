@@ -1,0 +1,38 @@
+// bm_config.hpp -- benchmark configuration for the XOR-EC HIP plugin.
+//
+// Mirrors the fields and meaning of the reference's BenchmarkConfig
+// (src/benchmark/bm_config.hpp:25-43) so a config built for the reference's
+// "xorec-gpu" plugin means the same thing here.  Fields that only exist for
+// the reference's CUDA launch (num_gpu_blocks / threads_per_gpu_block) are kept
+// for the CSV schema; the HIP path chooses its own launch shape.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <tuple>
+
+namespace xec {
+
+using ECTuple = std::tuple<size_t, size_t>;  // (total blocks, data blocks), bm_config.hpp:18
+
+struct BenchmarkConfig {
+  size_t message_size = 0;      // bytes of data per batch (all stripes)
+  size_t block_size = 0;        // bytes per block (shard)
+  ECTuple ec_params{0, 0};      // (k + m, k)
+  size_t num_lost_blocks = 0;   // lost blocks per stripe (data or parity)
+  size_t num_cpu_threads = 1;   // host threads for setup / validation
+  int num_iterations = 10;      // timed iterations (benchmark_suite.cpp:30)
+  int num_warmup_iterations = 0;
+  bool gpu_computation = true;
+  size_t num_gpu_blocks = 0;          // CSV only (reference launch grid)
+  size_t threads_per_gpu_block = 256; // CSV only
+  int device_id = 0;            // new: HIP device of this process
+  uint64_t seed = 0;            // new: explicit seed (reference seeds from the clock)
+};
+
+inline size_t data_blocks(const BenchmarkConfig& c) { return std::get<1>(c.ec_params); }
+inline size_t parity_blocks(const BenchmarkConfig& c) {
+  return std::get<0>(c.ec_params) - std::get<1>(c.ec_params);
+}
+
+}  // namespace xec

@@ -1,0 +1,98 @@
+// xec_bench.cpp -- command-line harness: the reference's "xorec-gpu" benchmark
+// (BM_XOREC_GPU_CMP, src/benchmark/runners.cpp:43-45) re-registered as
+// "xorec-hip", one CSV row per configuration in the reference's schema.
+//
+//   xec_bench [-s message_bytes] [-b block_bytes] [-k data] [-m parity]
+//             [-l lost_per_stripe] [-i iterations] [-w warmup] [-t cpu_threads]
+//             [-d device] [-r seed] [-o out.csv] [--no-header]
+// Sizes accept K/M/G suffixes (binary).  Defaults: BASELINE.json configs[2]
+// (k=16+1, 1 MiB blocks, 256 stripes = 4 GiB message), 1 lost block, 10
+// iterations, 0 warm-up (the reference's defaults, benchmark_suite.cpp:30-31).
+#include <omp.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+
+#include "runner.hpp"
+#include "xorec_hip_bm.hpp"
+
+namespace {
+
+size_t parse_size(const char* s) {
+  char* end = nullptr;
+  unsigned long long v = std::strtoull(s, &end, 0);
+  switch (end && *end ? *end : 0) {
+    case 'K': case 'k': v <<= 10; break;
+    case 'M': v <<= 20; break;
+    case 'G': case 'g': v <<= 30; break;
+    default: break;
+  }
+  return static_cast<size_t>(v);
+}
+
+void usage() {
+  std::fprintf(stderr,
+               "usage: xec_bench [-s message_bytes] [-b block_bytes] [-k data] [-m parity]\n"
+               "                 [-l lost] [-i iters] [-w warmup] [-t threads] [-d device]\n"
+               "                 [-r seed] [-o out.csv] [--no-header]\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  xec::BenchmarkConfig cfg;
+  size_t k = 16, m = 1;
+  cfg.block_size = 1 << 20;
+  cfg.message_size = 256ull * 16 * (1 << 20);
+  cfg.num_lost_blocks = 1;
+  cfg.num_cpu_threads = static_cast<size_t>(omp_get_max_threads());
+  std::string out;
+  bool header = true;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&]() -> const char* {
+      if (i + 1 >= argc) { usage(); std::exit(2); }
+      return argv[++i];
+    };
+    if (a == "-s") cfg.message_size = parse_size(val());
+    else if (a == "-b") cfg.block_size = parse_size(val());
+    else if (a == "-k") k = parse_size(val());
+    else if (a == "-m") m = parse_size(val());
+    else if (a == "-l") cfg.num_lost_blocks = parse_size(val());
+    else if (a == "-i") cfg.num_iterations = std::atoi(val());
+    else if (a == "-w") cfg.num_warmup_iterations = std::atoi(val());
+    else if (a == "-t") cfg.num_cpu_threads = parse_size(val());
+    else if (a == "-d") cfg.device_id = std::atoi(val());
+    else if (a == "-r") cfg.seed = parse_size(val());
+    else if (a == "-o") out = val();
+    else if (a == "--no-header") header = false;
+    else if (a == "-h" || a == "--help") { usage(); return 0; }
+    else { usage(); return 2; }
+  }
+  cfg.ec_params = {k + m, k};
+  if (cfg.num_lost_blocks > m) {
+    // the reference prints and exits (utils.cpp:102-105)
+    std::fprintf(stderr, "lost blocks per stripe (%zu) must be <= parity blocks (%zu)\n",
+                 cfg.num_lost_blocks, m);
+    return 2;
+  }
+  try {
+    xec::RunResult r = xec::run_generic<xec::XorecBenchmarkHip>("XOR-EC (HIP gfx950)", cfg);
+    std::ofstream f;
+    std::ostream* os = &std::cout;
+    if (!out.empty()) {
+      f.open(out, std::ios::app);
+      os = &f;
+    }
+    if (header) xec::write_csv_header(*os);
+    xec::write_csv_row(*os, r, cfg);
+    return r.err_msg.empty() ? 0 : 1;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "xec_bench: %s\n", e.what());
+    return 3;
+  }
+}

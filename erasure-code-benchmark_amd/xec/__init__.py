@@ -5,12 +5,12 @@ of include/xec.h).  This package only binds it for tests, bench.py and the
 multi-GPU partitioning helpers; it never computes parity itself.
 """
 from ._lib import EXPORTED, LIB_PATH, Status, XecLibraryError, lib
-from .codec import (build_info, check_args, check_bitmap, decode, encode, erase, fill_splitmix64,
-                    init, set_launch, status_string)
+from .codec import (Pipeline, build_info, check_args, check_bitmap, decode, encode, erase,
+                    fill_splitmix64, init, set_launch, status_string)
 from .partition import stripe_range
 
 __all__ = [
-    "EXPORTED", "LIB_PATH", "Status", "XecLibraryError", "lib", "build_info", "check_args",
-    "check_bitmap", "decode", "encode", "erase", "fill_splitmix64", "init", "set_launch",
-    "status_string", "stripe_range",
+    "EXPORTED", "LIB_PATH", "Pipeline", "Status", "XecLibraryError", "lib", "build_info",
+    "check_args", "check_bitmap", "decode", "encode", "erase", "fill_splitmix64", "init",
+    "set_launch", "status_string", "stripe_range",
 ]

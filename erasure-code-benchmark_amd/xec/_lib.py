@@ -23,7 +23,8 @@ LIB_PATH = Path(os.environ.get("XEC_LIB", Path(__file__).resolve().parent / LIB_
 EXPORTED = (
     "xec_init", "xec_encode", "xec_decode", "xec_check_bitmap", "xec_check_args",
     "xec_erase", "xec_fill_splitmix64", "xec_set_launch", "xec_status_string",
-    "xec_build_info",
+    "xec_build_info", "xec_pipeline_create", "xec_pipeline_destroy", "xec_pipeline_encode",
+    "xec_pipeline_decode",
 )
 
 
@@ -78,6 +79,10 @@ def lib() -> ctypes.CDLL:
         "xec_set_launch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], st),
         "xec_status_string": ([st], ctypes.c_char_p),
         "xec_build_info": ([], ctypes.c_char_p),
+        "xec_pipeline_create": ([ctypes.POINTER(vp), sz, sz, sz, sz, ctypes.c_int], st),
+        "xec_pipeline_destroy": ([vp], st),
+        "xec_pipeline_encode": ([vp, vp, vp, sz], st),
+        "xec_pipeline_decode": ([vp, vp, vp, sz, vp], st),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

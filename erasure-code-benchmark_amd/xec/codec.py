@@ -82,3 +82,43 @@ def status_string(st: int) -> str:
 
 def build_info() -> str:
     return lib().xec_build_info().decode()
+
+
+class Pipeline:
+    """Host-in / host-out encoder-decoder (xec_pipeline_*, include/xec.h).
+
+    Owns ``nstreams`` device slots of ``chunk_stripes`` stripes on the current
+    device; host buffers (numpy arrays, pinned torch tensors or addresses) are
+    streamed through them.  Use as a context manager or call :meth:`close`."""
+
+    def __init__(self, chunk_stripes: int, bs: int, k: int, m: int, nstreams: int = 2):
+        self.bs, self.k, self.m = bs, k, m
+        h = ctypes.c_void_p()
+        st = Status(lib().xec_pipeline_create(ctypes.byref(h), chunk_stripes, bs, k, m, nstreams))
+        if st != Status.SUCCESS:
+            raise RuntimeError(f"xec_pipeline_create failed: {st!r}")
+        self._h = h
+
+    def encode(self, h_data, h_parity, S: int) -> Status:
+        return Status(lib().xec_pipeline_encode(self._h, _ptr(h_data), _ptr(h_parity), S))
+
+    def decode(self, h_data, h_parity, S: int, h_bitmap) -> Status:
+        return Status(lib().xec_pipeline_decode(self._h, _ptr(h_data), _ptr(h_parity), S,
+                                                _ptr(h_bitmap)))
+
+    def close(self) -> None:
+        if self._h:
+            lib().xec_pipeline_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter teardown
+            pass

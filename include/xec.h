@@ -110,6 +110,31 @@ xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint6
  *   cache_policy 1 = non-temporal loads/stores (nt), 2 = default policy. */
 xec_status xec_set_launch(int unroll, int max_grid, int cache_policy);
 
+/* ---- host-in / host-out pipeline --------------------
+ * The MI355X analogue of the reference's GPU-memory / unified-memory variants
+ * (src/algorithms/xorec_gpu_ptr_bm.cpp:17-65, xorec_unified_ptr_bm.cpp:15-86,
+ * src/xorec/xorec.cpp:114-320), which keep the data on the host side of the
+ * link.  A pipeline owns `nstreams` (1..16) device slots of `chunk_stripes`
+ * stripes on the current device; a batch in host memory is streamed through
+ * them chunk by chunk: H2D -> kernel -> D2H, chunks overlapping across
+ * streams.  Host buffers should be pinned (hipHostMalloc / registered) for the
+ * copies to be asynchronous; the calls return when the results are in host
+ * memory.  Same argument checks and status codes as xec_encode / xec_decode. */
+typedef struct xec_pipeline xec_pipeline;
+
+xec_status xec_pipeline_create(xec_pipeline** out, size_t chunk_stripes, size_t bs, size_t k,
+                               size_t m, int nstreams);
+xec_status xec_pipeline_destroy(xec_pipeline* p);
+
+/* h_data: S*k*bs bytes in, h_parity: S*m*bs bytes out. */
+xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_parity, size_t S);
+
+/* Rebuilds lost data blocks of h_data in place from h_parity (read-only);
+ * only chunks that lost a data block cross the link, and only the rebuilt
+ * blocks are copied back.  All-or-nothing like xec_decode. */
+xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_parity, size_t S,
+                               const uint8_t* h_bitmap);
+
 /* Human-readable status name ("Success", "InvalidSize", ...). */
 const char* xec_status_string(xec_status s);
 
