@@ -25,23 +25,25 @@ std::atomic<bool> g_initialised{false};
 std::atomic<int> g_unroll{0};
 std::atomic<int> g_max_grid{0};
 std::atomic<int> g_nt{0};
+std::atomic<int> g_threads{0};
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
 constexpr size_t kAlign = 64;           // XOREC_ALIGNMENT
 
-// Defaults measured on MI355X (tools/sweep.py, profiles/sweep_*.json):
-// non-temporal loads and stores win for both kernels (every byte is touched
-// once); encode prefers one workgroup per 4 KiB tile, decode amortises its
-// bitmap lookup over 8 KiB tiles in a 4096-workgroup grid-stride launch.
-xec::LaunchShape launch_shape(size_t bs, bool decode) {
+// Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
+// non-temporal loads and stores (every byte is touched once), one-wave
+// workgroups with one 1 KiB tile each, one workgroup per tile.
+xec::LaunchShape launch_shape(size_t bs) {
   xec::LaunchShape ls;
-  int u = g_unroll.load(std::memory_order_relaxed);
-  if (u != 1 && u != 2 && u != 4) u = (decode && bs / 16 >= 2u * xec::kThreads) ? 2 : 1;
-  ls.unroll = u;
-  int g = g_max_grid.load(std::memory_order_relaxed);
-  ls.max_grid = g > 0 ? (uint32_t)g : (decode ? 4096u : 0u);
-  ls.nt = g_nt.load(std::memory_order_relaxed) != 2;
+  const int t = g_threads.load(std::memory_order_relaxed);
+  ls.threads = t == 256 ? 256 : 64;
+  const int u = g_unroll.load(std::memory_order_relaxed);
+  ls.unroll = (u == 1 || u == 2) ? u : 1;
+  const int g = g_max_grid.load(std::memory_order_relaxed);
+  ls.max_grid = g > 0 ? (uint32_t)g : 0u;
+  // nt stores address the block with a 32-bit buffer offset (xec_kernels.hip)
+  ls.nt = g_nt.load(std::memory_order_relaxed) != 2 && bs <= 0x7fffffffu;
   return ls;
 }
 
@@ -127,8 +129,8 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
-  xec::LaunchShape ls = launch_shape(bs, false);
-  xec::Geometry g = xec::make_geometry(S, bs, k, m, ls.unroll);
+  const xec::LaunchShape ls = launch_shape(bs);
+  const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   return xec::launch_encode(d_data, d_parity, g, ls, stream) == hipSuccess ? XEC_SUCCESS
                                                                            : XEC_DEVICE_ERROR;
 }
@@ -146,8 +148,8 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   if (hipMemcpyAsync(d_bitmap, h_bitmap, S * (k + m), hipMemcpyHostToDevice, stream) !=
       hipSuccess)
     return XEC_DEVICE_ERROR;
-  xec::LaunchShape ls = launch_shape(bs, true);
-  xec::Geometry g = xec::make_geometry(S, bs, k, m, ls.unroll);
+  const xec::LaunchShape ls = launch_shape(bs);
+  const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
              ? XEC_SUCCESS
              : XEC_DEVICE_ERROR;
@@ -159,7 +161,7 @@ xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
-  xec::Geometry g = xec::make_geometry(S, bs, k, m, 1);
+  const xec::Geometry g = xec::make_geometry(S, bs, k, m, xec::LaunchShape{256, 1, 0, false});
   return xec::launch_erase(d_data, d_parity, d_bitmap, g, stream) == hipSuccess ? XEC_SUCCESS
                                                                                : XEC_DEVICE_ERROR;
 }
@@ -174,9 +176,11 @@ xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint6
              : XEC_DEVICE_ERROR;
 }
 
-xec_status xec_set_launch(int unroll, int max_grid, int cache_policy) {
-  if (unroll != 0 && unroll != 1 && unroll != 2 && unroll != 4) return XEC_INVALID_SIZE;
+xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_threads) {
+  if (unroll != 0 && unroll != 1 && unroll != 2) return XEC_INVALID_SIZE;
   if (max_grid < 0 || cache_policy < 0 || cache_policy > 2) return XEC_INVALID_SIZE;
+  if (block_threads != 0 && block_threads != 64 && block_threads != 256) return XEC_INVALID_SIZE;
+  g_threads.store(block_threads, std::memory_order_relaxed);
   g_unroll.store(unroll, std::memory_order_relaxed);
   g_max_grid.store(max_grid, std::memory_order_relaxed);
   g_nt.store(cache_policy, std::memory_order_relaxed);

@@ -7,39 +7,40 @@
 
 namespace xec {
 
-constexpr int kThreads = 256;  // 4 waves of 64 lanes per workgroup
-
-// Batch geometry, all in 16-byte granules except where named *_bytes.
+// Batch geometry.  A tile is one class of one stripe over threads*unroll
+// 16-byte granules of the block.
 struct Geometry {
   uint64_t S;                // stripes
   uint64_t k, m, nm;         // data blocks, parity blocks, members per class (k/m)
-  uint64_t gran;             // granules per block (bs / 16)
-  uint64_t tiles_per_block;  // ceil(gran / (kThreads * unroll))
+  uint64_t bs;               // bytes per block
+  uint64_t tiles_per_block;  // ceil(bs / (16 * threads * unroll))
   uint64_t total_tiles;      // S * m * tiles_per_block
 };
 
 struct LaunchShape {
-  int unroll;         // granules per thread per member: 1, 2 or 4
-  uint32_t max_grid;  // 0 = one workgroup per tile
+  int threads;        // workgroup size: 64 (one wave) or 256
+  int unroll;         // granules per lane per class member: 1 or 2
+  uint32_t max_grid;  // 0 = one workgroup per tile, else grid-stride over tiles
   bool nt;            // non-temporal loads/stores
 };
 
-inline Geometry make_geometry(uint64_t S, uint64_t bs, uint64_t k, uint64_t m, int unroll) {
+inline Geometry make_geometry(uint64_t S, uint64_t bs, uint64_t k, uint64_t m,
+                              const LaunchShape& ls) {
   Geometry g;
   g.S = S;
   g.k = k;
   g.m = m;
   g.nm = k / m;
-  g.gran = bs / 16;
-  uint64_t tile = (uint64_t)kThreads * (uint64_t)unroll;
-  g.tiles_per_block = (g.gran + tile - 1) / tile;
+  g.bs = bs;
+  const uint64_t tile_bytes = 16ull * (uint64_t)ls.threads * (uint64_t)ls.unroll;
+  g.tiles_per_block = (bs + tile_bytes - 1) / tile_bytes;
   g.total_tiles = S * m * g.tiles_per_block;
   return g;
 }
 
 inline uint32_t grid_for(uint64_t work_items, uint32_t max_grid) {
-  uint64_t cap = max_grid ? (uint64_t)max_grid : (uint64_t)0x7fffffffu;
-  uint64_t grid = work_items < cap ? work_items : cap;
+  const uint64_t cap = max_grid ? (uint64_t)max_grid : (uint64_t)0x7fffffffu;
+  const uint64_t grid = work_items < cap ? work_items : cap;
   return (uint32_t)(grid ? grid : 1);
 }
 

@@ -6,15 +6,21 @@
 // 8-byte grid-stride loop here (cf. xorec_gpu_cmp.cu:119-208).
 //
 // Work unit ("tile"): one parity class j of one stripe c over a contiguous
-// column range of 256*U 16-byte granules.  A thread owns U granules of the
-// column range and keeps every member of the class in flight at once:
+// column range of T*U 16-byte granules (T = threads per workgroup, 64 or 256).
+// A lane owns U granules of the column range and keeps every member of the
+// class in flight at once:
 //   encode: NM = k/m loads  (data blocks j, j+m, ...)      -> 1 parity store
 //   decode: NM loads        (class members, lost one       -> 1 store into the
 //                            replaced by the class parity)     lost data block
 // so each wave-instruction is a fully coalesced 1 KiB global_load_dwordx4
 // from one block and each lane has NM*U independent 16-byte loads in flight.
 // The XOR reduction happens in registers; no LDS is needed because no byte is
-// read twice and no cross-lane exchange is needed (see DESIGN.md, "Why no LDS").
+// read twice and no cross-lane exchange is needed (DESIGN.md, "Why no LDS").
+//
+// Addresses are formed per load as (uniform block base) + r*stride + (lane
+// offset) in 64-bit VGPR arithmetic.  Keeping an array of NM uniform member
+// pointers instead costs ~2*NM SGPRs; above 80 SGPRs gfx950 admits one wave
+// per SIMD fewer (MI355X_MICROARCH.md, Residency), which measured -5 % here.
 //
 // All byte offsets are 64-bit: the batch may exceed 4 GiB (cf. the 32-bit
 // indices of xorec_gpu_cmp.cu:127-131).
@@ -26,21 +32,42 @@
 namespace xec {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+// pointer into the constant address space: uniform loads through it become
+// scalar (s_load) loads served by the scalar cache
+typedef const uint32_t __attribute__((address_space(4)))* const_u32_as4;
 
 template <bool NT>
-__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
 }
 
 template <bool NT>
-__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+  u32x4* q = reinterpret_cast<u32x4*>(p);
+  if constexpr (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
 }
 
-// Decompose a tile index into (stripe c, class j, column chunk).
+// Store 16 bytes at block + off.  With NT the store is a buffer store whose
+// cache policy is an explicit operand (aux 2 = nt): hipcc (ROCm 7.2) silently
+// drops the !nontemporal of __builtin_nontemporal_store in the unrolled
+// reduction below (the emitted global_store has no `nt`), which measured 5 %
+// slower.  tests/test_isa.py checks every NT kernel's stores carry nt.
+template <bool NT>
+__device__ __forceinline__ void st16_block(uint8_t* block, uint64_t off, u32x4 v) {
+  if constexpr (NT) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(block, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)off, 0, 2);
+  } else {
+    st16<false>(block + off, v);
+  }
+}
+
+// Decompose a tile index into (stripe c, class j, column chunk); chunks of
+// one block are adjacent tile indices.
 struct TileCoord {
   uint64_t c, j, chunk;
 };
@@ -48,89 +75,77 @@ struct TileCoord {
 __device__ __forceinline__ TileCoord tile_coord(uint64_t t, const Geometry& g) {
   TileCoord tc;
   tc.chunk = t % g.tiles_per_block;
-  uint64_t cj = t / g.tiles_per_block;
+  const uint64_t cj = t / g.tiles_per_block;
   tc.j = cj % g.m;
   tc.c = cj / g.m;
   return tc;
 }
 
-// XOR-reduce NM members (base + r*stride for r != subst, `sub` for r == subst)
-// over this thread's U granules starting at granule offset g0, and store into
-// dst.  `full` = every granule of the tile lies inside the block.
-template <int NM, int U, bool NT>
-__device__ __forceinline__ void reduce_store(const u32x4* base, uint64_t stride, const u32x4* sub,
-                                             int subst, u32x4* dst, uint64_t g0, uint64_t gran,
-                                             uint32_t nm_rt) {
-  constexpr int kT = kThreads;
+// XOR-reduce the NM members of one class over this lane's U granules and
+// store the result at dst.  Member r lives at base + r*stride, except member
+// `subst`, whose bytes come from `sub` instead (decode: the class parity).
+// `off` = this lane's byte offset of granule 0 in the block; granule u is
+// off + u*T*16 and takes part only while inside the block (ragged tiles).
+template <int NM, int U, bool NT, int T>
+__device__ __forceinline__ void xor_members(const uint8_t* base, uint64_t stride,
+                                            const uint8_t* sub, int subst, uint8_t* dst,
+                                            uint64_t off, uint64_t bs, uint32_t nm_rt) {
+  constexpr uint64_t kStep = (uint64_t)T * 16;
   if constexpr (NM > 0) {
-    const u32x4* src[NM];
-#pragma unroll
-    for (int r = 0; r < NM; ++r) src[r] = (r == subst) ? sub : base + (uint64_t)r * stride;
-    if (g0 + (uint64_t)(U - 1) * kT < gran) {
+    if (off + (U - 1) * kStep < bs) {  // whole tile inside the block: no predication
       u32x4 v[NM][U];
 #pragma unroll
-      for (int r = 0; r < NM; ++r)
+      for (int r = 0; r < NM; ++r) {
+        const uint8_t* src = (r == subst ? sub : base + (uint64_t)r * stride) + off;
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[r][u] = ld16<NT>(src[r] + g0 + u * kT);
+        for (int u = 0; u < U; ++u) v[r][u] = ld16<NT>(src + u * kStep);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         u32x4 acc = v[0][u];
 #pragma unroll
         for (int r = 1; r < NM; ++r) acc ^= v[r][u];
-        st16<NT>(dst + g0 + u * kT, acc);
+        st16_block<NT>(dst, off + u * kStep, acc);
       }
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        uint64_t gi = g0 + u * kT;
-        if (gi < gran) {
-          u32x4 acc = ld16<NT>(src[0] + gi);
-#pragma unroll
-          for (int r = 1; r < NM; ++r) acc ^= ld16<NT>(src[r] + gi);
-          st16<NT>(dst + gi, acc);
-        }
-      }
+      return;
     }
-  } else {
-    // Runtime member count: groups of 8 loads in flight per granule.
+  }
+  // Ragged tail of a block, or a member count without a compiled unroll
+  // (groups of 8 loads in flight per granule).
+  const uint32_t nm = NM > 0 ? (uint32_t)NM : nm_rt;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      uint64_t gi = g0 + u * kT;
-      if (gi >= gran) continue;
-      u32x4 acc = {0u, 0u, 0u, 0u};
-      uint32_t r = 0;
-      for (; r + 8 <= nm_rt; r += 8) {
-        u32x4 v[8];
+  for (int u = 0; u < U; ++u) {
+    const uint64_t o = off + u * kStep;
+    if (o >= bs) continue;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    uint32_t r = 0;
+    for (; r + 8 <= nm; r += 8) {
+      u32x4 v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          int rr = (int)(r + q);
-          const u32x4* s = (rr == subst) ? sub : base + (uint64_t)rr * stride;
-          v[q] = ld16<NT>(s + gi);
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc ^= v[q];
+      for (int q = 0; q < 8; ++q) {
+        const int rr = (int)(r + q);
+        v[q] = ld16<NT>((rr == subst ? sub : base + (uint64_t)rr * stride) + o);
       }
-      for (; r < nm_rt; ++r) {
-        const u32x4* s = ((int)r == subst) ? sub : base + (uint64_t)r * stride;
-        acc ^= ld16<NT>(s + gi);
-      }
-      st16<NT>(dst + gi, acc);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc ^= v[q];
     }
+    for (; r < nm; ++r) acc ^= ld16<NT>(((int)r == subst ? sub : base + (uint64_t)r * stride) + o);
+    st16_block<NT>(dst, o, acc);
   }
 }
 
 // ---------------------------------------------------------------------------
 // encode: parity[c][j] = XOR_{r < k/m} data[c][j + r*m]      (xorec.cpp:37-57)
 // ---------------------------------------------------------------------------
-template <int NM, int U, bool NT>
-__global__ __launch_bounds__(kThreads) void encode_kernel(const u32x4* __restrict__ data,
-                                                          u32x4* __restrict__ parity, Geometry g) {
+template <int NM, int U, bool NT, int T>
+__global__ __launch_bounds__(T) void encode_kernel(const uint8_t* __restrict__ data,
+                                                   uint8_t* __restrict__ parity, Geometry g) {
   for (uint64_t t = blockIdx.x; t < g.total_tiles; t += gridDim.x) {
-    TileCoord tc = tile_coord(t, g);
-    const u32x4* base = data + (tc.c * g.k + tc.j) * g.gran;
-    u32x4* dst = parity + (tc.c * g.m + tc.j) * g.gran;
-    uint64_t g0 = tc.chunk * (uint64_t)(kThreads * U) + threadIdx.x;
-    reduce_store<NM, U, NT>(base, g.m * g.gran, nullptr, -1, dst, g0, g.gran, (uint32_t)g.nm);
+    const TileCoord tc = tile_coord(t, g);
+    const uint8_t* base = data + (tc.c * g.k + tc.j) * g.bs;
+    uint8_t* dst = parity + (tc.c * g.m + tc.j) * g.bs;
+    const uint64_t off = (tc.chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+    xor_members<NM, U, NT, T>(base, g.m * g.bs, nullptr, -1, dst, off, g.bs, (uint32_t)g.nm);
   }
 }
 
@@ -138,53 +153,68 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(const u32x4* __restric
 // decode: for the (at most one, checked on the host) lost data block L of
 // class j: data[c][L] = parity[c][j] ^ XOR_{r != L} data[c][j + r*m]
 //                                                            (xorec.cpp:79-108)
-// The lost member is found with one byte load per lane and a wave ballot.
+// The lost member is found from the class's bitmap bytes with scalar loads
+// (compiled member counts) or one byte load per lane and a wave ballot
+// (runtime member counts); every wave does this itself (no LDS, no barrier).
+// The scalar path reads the aligned dword containing each byte: it cannot
+// cross a page, so it never faults past the end of the caller's scratch.
 // ---------------------------------------------------------------------------
-template <int NM, int U, bool NT>
-__global__ __launch_bounds__(kThreads) void decode_kernel(u32x4* data,
-                                                          const u32x4* __restrict__ parity,
-                                                          const uint8_t* __restrict__ bitmap,
-                                                          Geometry g) {
+template <int NM, int U, bool NT, int T>
+__global__ __launch_bounds__(T) void decode_kernel(uint8_t* data, const uint8_t* __restrict__ parity,
+                                                   const uint8_t* __restrict__ bitmap, Geometry g) {
   const uint32_t nm = NM > 0 ? (uint32_t)NM : (uint32_t)g.nm;
   const uint32_t lane = threadIdx.x & 63u;
   for (uint64_t t = blockIdx.x; t < g.total_tiles; t += gridDim.x) {
-    TileCoord tc = tile_coord(t, g);
-    const uint8_t* row = bitmap + tc.c * (g.k + g.m);
+    const TileCoord tc = tile_coord(t, g);
+    const uint8_t* row = bitmap + tc.c * (g.k + g.m) + tc.j;
     int lost = -1;
-    for (uint32_t b = 0; b < nm; b += 64) {
-      uint32_t r = b + lane;
-      bool z = (r < nm) && (row[tc.j + (uint64_t)r * g.m] == 0);
-      uint64_t mask = __ballot(z);
-      if (mask) {
-        lost = (int)(b + (uint32_t)__builtin_ctzll(mask));
-        break;
+    if constexpr (NM > 0) {
+      // Scalar path: the class's bitmap bytes come through the scalar cache
+      // (one s_load_dword each, issued back to back), no vector round trip
+      // before the data loads can start (measured +3 % over the ballot).
+      // Absolute addresses: the caller's scratch pointer need not be aligned.
+      const uint64_t rowaddr = reinterpret_cast<uint64_t>(row);
+#pragma unroll
+      for (int r = NM - 1; r >= 0; --r) {
+        const uint64_t a = rowaddr + (uint64_t)r * g.m;
+        const uint32_t w = *(const_u32_as4)(a & ~3ull);
+        if (((w >> (8 * (a & 3))) & 0xffu) == 0) lost = r;
+      }
+    } else {
+      for (uint32_t b = 0; b < nm; b += 64) {
+        const uint32_t r = b + lane;
+        const bool z = (r < nm) && (row[(uint64_t)r * g.m] == 0);
+        const uint64_t mask = __ballot(z);
+        if (mask) {
+          lost = (int)(b + (uint32_t)__builtin_ctzll(mask));
+          break;
+        }
       }
     }
     lost = __builtin_amdgcn_readfirstlane(lost);
     if (lost < 0) continue;
-    u32x4* base = data + (tc.c * g.k + tc.j) * g.gran;
-    const uint64_t stride = g.m * g.gran;
-    const u32x4* par = parity + (tc.c * g.m + tc.j) * g.gran;
-    u32x4* dst = base + (uint64_t)lost * stride;
-    uint64_t g0 = tc.chunk * (uint64_t)(kThreads * U) + threadIdx.x;
-    reduce_store<NM, U, NT>(base, stride, par, lost, dst, g0, g.gran, nm);
+    uint8_t* base = data + (tc.c * g.k + tc.j) * g.bs;
+    const uint64_t stride = g.m * g.bs;
+    const uint8_t* par = parity + (tc.c * g.m + tc.j) * g.bs;
+    const uint64_t off = (tc.chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+    xor_members<NM, U, NT, T>(base, stride, par, lost, base + (uint64_t)lost * stride, off, g.bs,
+                              nm);
   }
 }
 
 // ---------------------------------------------------------------------------
 // erase: zero every block whose bitmap byte is 0 (abstract_bm.cpp:20-39)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void erase_kernel(u32x4* data, u32x4* parity,
-                                                         const uint8_t* __restrict__ bitmap,
-                                                         Geometry g) {
+__global__ __launch_bounds__(256) void erase_kernel(uint8_t* data, uint8_t* parity,
+                                                    const uint8_t* __restrict__ bitmap, Geometry g) {
   const uint64_t tot = g.k + g.m;
   const uint64_t nblocks = g.S * tot;
   const u32x4 zero = {0u, 0u, 0u, 0u};
   for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
     if (bitmap[b] != 0) continue;
-    uint64_t c = b / tot, i = b % tot;
-    u32x4* blk = i < g.k ? data + (c * g.k + i) * g.gran : parity + (c * g.m + (i - g.k)) * g.gran;
-    for (uint64_t x = threadIdx.x; x < g.gran; x += kThreads) blk[x] = zero;
+    const uint64_t c = b / tot, i = b % tot;
+    uint8_t* blk = i < g.k ? data + (c * g.k + i) * g.bs : parity + (c * g.m + (i - g.k)) * g.bs;
+    for (uint64_t x = threadIdx.x * 16ull; x < g.bs; x += 256 * 16) st16<false>(blk + x, zero);
   }
 }
 
@@ -198,13 +228,13 @@ __device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t n) {
   return z ^ (z >> 31);
 }
 
-__global__ __launch_bounds__(kThreads) void fill_kernel(uint64_t* buf, uint64_t S, uint64_t words,
-                                                        uint64_t seed_base) {
+__global__ __launch_bounds__(256) void fill_kernel(uint64_t* buf, uint64_t S, uint64_t words,
+                                                   uint64_t seed_base) {
   for (uint64_t c = blockIdx.y; c < S; c += gridDim.y) {
     uint64_t* row = buf + c * words;
     const uint64_t seed = seed_base + c;
-    for (uint64_t n = (uint64_t)blockIdx.x * kThreads + threadIdx.x; n < words;
-         n += (uint64_t)gridDim.x * kThreads)
+    for (uint64_t n = (uint64_t)blockIdx.x * 256 + threadIdx.x; n < words;
+         n += (uint64_t)gridDim.x * 256)
       row[n] = splitmix_at(seed, n);
   }
 }
@@ -214,84 +244,99 @@ __global__ __launch_bounds__(kThreads) void fill_kernel(uint64_t* buf, uint64_t 
 // ---------------------------------------------------------------------------
 namespace {
 
-template <int NM, int U, bool NT>
+template <int NM, int U, bool NT, int T>
 hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t grid,
                            hipStream_t s) {
-  encode_kernel<NM, U, NT><<<grid, kThreads, 0, s>>>(static_cast<const u32x4*>(d),
-                                                     static_cast<u32x4*>(p), g);
+  encode_kernel<NM, U, NT, T><<<grid, T, 0, s>>>(static_cast<const uint8_t*>(d),
+                                                 static_cast<uint8_t*>(p), g);
   return hipGetLastError();
 }
 
-template <int NM, int U, bool NT>
+template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
                            uint32_t grid, hipStream_t s) {
-  decode_kernel<NM, U, NT><<<grid, kThreads, 0, s>>>(static_cast<u32x4*>(d),
-                                                     static_cast<const u32x4*>(p), bm, g);
+  decode_kernel<NM, U, NT, T><<<grid, T, 0, s>>>(static_cast<uint8_t*>(d),
+                                                 static_cast<const uint8_t*>(p), bm, g);
   return hipGetLastError();
 }
 
-// Dispatch over the member count (k/m) the reference configs use
-// (bm_config.cpp:7-11 and BASELINE.json: 1, 2, 4, 8, 16, 32), runtime otherwise.
-#define XEC_NM_SWITCH(NMV, CALL)      \
-  switch (NMV) {                      \
-    case 1: { constexpr int NM = 1; CALL; } \
-    case 2: { constexpr int NM = 2; CALL; } \
-    case 4: { constexpr int NM = 4; CALL; } \
-    case 8: { constexpr int NM = 8; CALL; } \
-    case 16: { constexpr int NM = 16; CALL; } \
-    case 32: { constexpr int NM = 32; CALL; } \
-    default: { constexpr int NM = 0; CALL; } \
+// Member counts (k/m) compiled fully unrolled: those of the reference's sweep
+// (bm_config.cpp:7-11) and BASELINE.json -- 1, 2, 4, 8, 16, 32; others run the
+// generic loop (NM = 0).
+#define XEC_NM_SWITCH(NMV, CALL)                  \
+  switch (NMV) {                                  \
+    case 1: { constexpr int NM = 1; CALL; }       \
+    case 2: { constexpr int NM = 2; CALL; }       \
+    case 4: { constexpr int NM = 4; CALL; }       \
+    case 8: { constexpr int NM = 8; CALL; }       \
+    case 16: { constexpr int NM = 16; CALL; }     \
+    case 32: { constexpr int NM = 32; CALL; }     \
+    default: { constexpr int NM = 0; CALL; }      \
   }
 
-template <bool NT>
-hipError_t launch_encode_nt(const void* d, void* p, const Geometry& g, int unroll, uint32_t grid,
-                            hipStream_t s) {
-  if (unroll == 4) { XEC_NM_SWITCH(g.nm, return (launch_encode_t<NM, 4, NT>(d, p, g, grid, s))) }
-  if (unroll == 2) { XEC_NM_SWITCH(g.nm, return (launch_encode_t<NM, 2, NT>(d, p, g, grid, s))) }
-  XEC_NM_SWITCH(g.nm, return (launch_encode_t<NM, 1, NT>(d, p, g, grid, s)))
+template <int U, bool NT, int T>
+hipError_t enc_nm(const void* d, void* p, const Geometry& g, uint32_t grid, hipStream_t s) {
+  XEC_NM_SWITCH(g.nm, return (launch_encode_t<NM, U, NT, T>(d, p, g, grid, s)))
 }
 
-template <bool NT>
-hipError_t launch_decode_nt(void* d, const void* p, const uint8_t* bm, const Geometry& g,
-                            int unroll, uint32_t grid, hipStream_t s) {
-  if (unroll == 4) { XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, 4, NT>(d, p, bm, g, grid, s))) }
-  if (unroll == 2) { XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, 2, NT>(d, p, bm, g, grid, s))) }
-  XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, 1, NT>(d, p, bm, g, grid, s)))
+template <int U, bool NT, int T>
+hipError_t dec_nm(void* d, const void* p, const uint8_t* bm, const Geometry& g, uint32_t grid,
+                  hipStream_t s) {
+  XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, grid, s)))
+}
+
+template <bool NT, int T>
+hipError_t enc_u(const void* d, void* p, const Geometry& g, int unroll, uint32_t grid,
+                 hipStream_t s) {
+  return unroll == 2 ? enc_nm<2, NT, T>(d, p, g, grid, s) : enc_nm<1, NT, T>(d, p, g, grid, s);
+}
+
+template <bool NT, int T>
+hipError_t dec_u(void* d, const void* p, const uint8_t* bm, const Geometry& g, int unroll,
+                 uint32_t grid, hipStream_t s) {
+  return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, grid, s)
+                     : dec_nm<1, NT, T>(d, p, bm, g, grid, s);
 }
 
 }  // namespace
 
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
                          const LaunchShape& ls, hipStream_t s) {
-  uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
-  return ls.nt ? launch_encode_nt<true>(d_data, d_parity, g, ls.unroll, grid, s)
-               : launch_encode_nt<false>(d_data, d_parity, g, ls.unroll, grid, s);
+  const uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
+  if (ls.threads == 256)
+    return ls.nt ? enc_u<true, 256>(d_data, d_parity, g, ls.unroll, grid, s)
+                 : enc_u<false, 256>(d_data, d_parity, g, ls.unroll, grid, s);
+  return ls.nt ? enc_u<true, 64>(d_data, d_parity, g, ls.unroll, grid, s)
+               : enc_u<false, 64>(d_data, d_parity, g, ls.unroll, grid, s);
 }
 
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
                          const Geometry& g, const LaunchShape& ls, hipStream_t s) {
-  uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
-  return ls.nt ? launch_decode_nt<true>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s)
-               : launch_decode_nt<false>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s);
+  const uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
+  if (ls.threads == 256)
+    return ls.nt ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s)
+                 : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s);
+  return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s)
+               : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s);
 }
 
 hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, const Geometry& g,
                         hipStream_t s) {
-  uint64_t nblocks = g.S * (g.k + g.m);
-  uint32_t grid = grid_for(nblocks, 65536);
-  erase_kernel<<<grid, kThreads, 0, s>>>(static_cast<u32x4*>(d_data),
-                                         static_cast<u32x4*>(d_parity), d_bitmap, g);
+  const uint64_t nblocks = g.S * (g.k + g.m);
+  const uint32_t grid = grid_for(nblocks, 65536);
+  erase_kernel<<<grid, 256, 0, s>>>(static_cast<uint8_t*>(d_data), static_cast<uint8_t*>(d_parity),
+                                    d_bitmap, g);
   return hipGetLastError();
 }
 
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,
                        hipStream_t s) {
-  uint64_t gx = (words + kThreads - 1) / kThreads;
+  uint64_t gx = (words + 255) / 256;
   if (gx > 1024) gx = 1024;
-  uint64_t gy = S < 65535 ? S : 65535;
+  const uint64_t gy = S < 65535 ? S : 65535;
   if (gx == 0 || gy == 0) return hipSuccess;
-  fill_kernel<<<dim3((uint32_t)gx, (uint32_t)gy), kThreads, 0, s>>>(static_cast<uint64_t*>(d_buf),
-                                                                   S, words, seed_base);
+  fill_kernel<<<dim3((uint32_t)gx, (uint32_t)gy), 256, 0, s>>>(static_cast<uint64_t*>(d_buf), S,
+                                                              words, seed_base);
   return hipGetLastError();
 }
 

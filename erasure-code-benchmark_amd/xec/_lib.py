@@ -76,7 +76,7 @@ def lib() -> ctypes.CDLL:
         "xec_check_args": ([vp, vp, sz, sz, sz], st),
         "xec_erase": ([vp, vp, sz, sz, sz, sz, vp, vp], st),
         "xec_fill_splitmix64": ([vp, sz, sz, ctypes.c_uint64, vp], st),
-        "xec_set_launch": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], st),
+        "xec_set_launch": ([ctypes.c_int] * 4, st),
         "xec_status_string": ([st], ctypes.c_char_p),
         "xec_build_info": ([], ctypes.c_char_p),
         "xec_pipeline_create": ([ctypes.POINTER(vp), sz, sz, sz, sz, ctypes.c_int], st),

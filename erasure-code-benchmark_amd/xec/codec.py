@@ -71,9 +71,11 @@ def check_args(data_addr: int, parity_addr: int, bs: int, k: int, m: int) -> Sta
     return Status(lib().xec_check_args(data_addr, parity_addr, bs, k, m))
 
 
-def set_launch(unroll: int = 0, max_grid: int = 0, cache_policy: int = 0) -> Status:
-    """xec_set_launch; 0 = default for each; cache_policy 1 = nt, 2 = default policy."""
-    return Status(lib().xec_set_launch(unroll, max_grid, cache_policy))
+def set_launch(unroll: int = 0, max_grid: int = 0, cache_policy: int = 0,
+               block_threads: int = 0) -> Status:
+    """xec_set_launch; 0 = default for each; cache_policy 1 = nt, 2 = default policy;
+    block_threads 64 or 256."""
+    return Status(lib().xec_set_launch(unroll, max_grid, cache_policy, block_threads))
 
 
 def status_string(st: int) -> str:

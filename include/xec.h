@@ -105,10 +105,11 @@ xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint6
 
 /* Launch-shape override for tuning sweeps (process-wide, not thread-safe
  * against concurrent launches).  Each argument 0 = the measured default:
- *   unroll       16-byte granules per thread per class member: 1, 2 or 4;
- *   max_grid     workgroups per launch (grid-stride beyond), 0 = one per tile;
- *   cache_policy 1 = non-temporal loads/stores (nt), 2 = default policy. */
-xec_status xec_set_launch(int unroll, int max_grid, int cache_policy);
+ *   unroll        16-byte granules per lane per class member: 1 or 2;
+ *   max_grid      workgroups per launch (grid-stride beyond), 0 = one per tile;
+ *   cache_policy  1 = non-temporal loads/stores (nt), 2 = default policy;
+ *   block_threads workgroup size, 64 (one wave) or 256. */
+xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_threads);
 
 /* ---- host-in / host-out pipeline --------------------
  * The MI355X analogue of the reference's GPU-memory / unified-memory variants

@@ -131,6 +131,9 @@ def test_check_bitmap_single_erasure_large():
 
 def test_set_launch_validation():
     assert xec.set_launch(3, 0, 0) == xec.Status.INVALID_SIZE
+    assert xec.set_launch(4, 0, 0) == xec.Status.INVALID_SIZE
     assert xec.set_launch(1, -1, 0) == xec.Status.INVALID_SIZE
     assert xec.set_launch(1, 0, 3) == xec.Status.INVALID_SIZE
-    assert xec.set_launch(0, 0, 0) == xec.Status.SUCCESS
+    assert xec.set_launch(1, 0, 0, 128) == xec.Status.INVALID_SIZE
+    assert xec.set_launch(2, 64, 1, 256) == xec.Status.SUCCESS
+    assert xec.set_launch(0, 0, 0, 0) == xec.Status.SUCCESS

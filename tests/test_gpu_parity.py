@@ -128,6 +128,25 @@ def test_edge_shapes_multi_erasure(gpu, oracle, S, k, m, bs):
     erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
 
 
+@pytest.mark.parametrize("misalign", [1, 2, 3, 5])
+@pytest.mark.parametrize("S,k,m,bs", [(9, 16, 1, 4096), (7, 16, 4, 2048), (5, 10, 2, 1024)])
+def test_unaligned_bitmap_scratch(gpu, oracle, misalign, S, k, m, bs):
+    """The device bitmap scratch is caller-owned and may sit at any byte address."""
+    torch = _torch()
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(S):
+        oracle.select_lost_blocks(k, m, m, bm[c], 31 + c)
+    bm = bm.reshape(-1)
+    h_bm = torch.from_numpy(bm).pin_memory()
+    d_bm = h_bm.to("cuda")
+    assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == 0
+    scratch = torch.full((bm.size + 16,), 0xFF, dtype=torch.uint8, device="cuda")
+    assert gpu.decode(b.d, b.p, S, bs, k, m, h_bm, scratch.data_ptr() + misalign,
+                      b.stream) == gpu.Status.SUCCESS
+    assert np.array_equal(b.data(), ref_d)
+
+
 def test_empty_batch_is_noop(gpu):
     torch = _torch()
     d = torch.empty(64, dtype=torch.uint8, device="cuda")
@@ -160,10 +179,11 @@ def test_argument_errors_launch_nothing(gpu):
     assert int(p.sum()) == 0
 
 
-@pytest.mark.parametrize("unroll", [1, 2, 4])
+@pytest.mark.parametrize("threads", [64, 256])
+@pytest.mark.parametrize("unroll", [1, 2])
 @pytest.mark.parametrize("max_grid,nt", [(0, 2), (0, 1), (300, 2), (2048, 1), (0, 0)])
-def test_launch_shapes_bit_exact(gpu, oracle, unroll, max_grid, nt):
-    assert gpu.set_launch(unroll, max_grid, nt) == gpu.Status.SUCCESS
+def test_launch_shapes_bit_exact(gpu, oracle, threads, unroll, max_grid, nt):
+    assert gpu.set_launch(unroll, max_grid, nt, threads) == gpu.Status.SUCCESS
     try:
         for (S, k, m, bs) in [(24, 16, 1, 65536), (40, 32, 4, 4352), (9, 10, 2, 2816)]:
             b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
@@ -172,7 +192,7 @@ def test_launch_shapes_bit_exact(gpu, oracle, unroll, max_grid, nt):
                 oracle.select_lost_blocks(k, m, m, bm[c], 77 + c)
             erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
     finally:
-        gpu.set_launch(0, 0, 0)
+        gpu.set_launch(0, 0, 0, 0)
 
 
 def test_encode_is_linear(gpu):

@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of experimental encode variants (tools/lab/liblab.so) against
+the product kernel, on one MI355X, HIP events on the launching stream.
+
+    python tools/lab/lab.py [--rounds 7] [--iters 10] [--variants 0,1,...] [--gap-ms 0]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--S", type=int, default=256)
+    ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--bs", type=int, default=1 << 20)
+    ap.add_argument("--gap-ms", type=float, default=0.0, help="host sleep between launches")
+    ap.add_argument("--out", default="")
+    ap.add_argument("--decode", action="store_true", help="time the decode diagnostics")
+    args = ap.parse_args()
+
+    import torch
+
+    import xec
+
+    torch.cuda.set_device(0)
+    assert xec.init(0) == 0
+    L = ctypes.CDLL(str(Path(__file__).resolve().parent / "liblab.so"))
+    L.lab_variant_name.restype = ctypes.c_char_p
+    L.lab_variant_name.argtypes = [ctypes.c_int]
+    L.lab_encode.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
+    names = {}
+    v = 0
+    while L.lab_variant_name(v):
+        names[v] = L.lab_variant_name(v).decode()
+        v += 1
+    chosen = [int(x) for x in args.variants.split(",")] if args.variants else sorted(names)
+
+    S, k, m, bs = args.S, args.k, 1, args.bs
+    s = torch.cuda.current_stream()
+    sh = s.cuda_stream
+    sets = []
+    for i in range(2):
+        d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+        p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+        assert xec.fill_splitmix64(d, S, k * bs, 1896 + 7919 * i, s) == 0
+        assert xec.encode(d, p, S, bs, k, m, s) == 0
+        sets.append((d, p))
+    torch.cuda.synchronize()
+    ref = [p.clone() for _, p in sets]
+    b_enc = S * (k + m) * bs
+
+    if args.decode:
+        return decode_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh)
+
+    # correctness of every variant first
+    bad = []
+    for v in chosen:
+        for i, (d, p) in enumerate(sets):
+            p.zero_()
+            assert L.lab_encode(v, d.data_ptr(), p.data_ptr(), S, bs, k, m, sh) == 0
+            torch.cuda.synchronize()
+            if not torch.equal(p, ref[i]):
+                bad.append(names[v])
+    print("incorrect variants:", bad, flush=True)
+
+    def run(fn):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.iters)]
+        fn(0)
+        ts = []
+        for i in range(args.iters):
+            if args.gap_ms:
+                torch.cuda.synchronize()
+                time.sleep(args.gap_ms * 1e-3)
+            ev[2 * i].record(s)
+            fn(i + 1)
+            ev[2 * i + 1].record(s)
+        torch.cuda.synchronize()
+        return [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.iters)]
+
+    res = {names[v]: [] for v in chosen}
+    res["product"] = []
+    for _ in range(args.rounds):
+        res["product"] += run(lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
+        for v in chosen:
+            res[names[v]] += run(lambda i, v=v: L.lab_encode(v, sets[i % 2][0].data_ptr(),
+                                                            sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
+    out = {}
+    for n, ts in res.items():
+        med = statistics.median(ts)
+        out[n] = {"ms_med": round(med, 4), "ms_min": round(min(ts), 4),
+                  "GBps_med": round(b_enc / (med * 1e-3) / 1e9, 1),
+                  "GBps_best": round(b_enc / (min(ts) * 1e-3) / 1e9, 1)}
+    for n, r in sorted(out.items(), key=lambda kv: -kv[1]["GBps_med"]):
+        print(f"{n:24s} {r}")
+    if args.out:
+        Path(args.out).write_text(json.dumps({"shape": [S, k, m, bs], "gap_ms": args.gap_ms,
+                                              "incorrect": bad, "results": out}, indent=1))
+
+
+
+def decode_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):
+    import numpy as np
+    L.lab_dec_name.restype = ctypes.c_char_p
+    L.lab_dec_name.argtypes = [ctypes.c_int]
+    L.lab_decode.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
+    names = {}
+    v = 0
+    while L.lab_dec_name(v):
+        names[v] = L.lab_dec_name(v).decode()
+        v += 1
+    lost = (7 * np.arange(S)) % k
+    bm = np.ones((S, k + m), np.uint8)
+    bm[np.arange(S), lost] = 0
+    h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
+    d_bm = h_bm.to("cuda")
+    table = torch.from_numpy(lost.astype(np.uint8)).to("cuda")
+    out = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+    ref = [d.clone() for d, _ in sets]
+    lookups = {v: (d_bm if v in (0, 5, 11) else table) for v in names}
+    bad = []
+    for v in names:
+        for i, (d, p) in enumerate(sets):
+            assert xec.erase(d, p, S, bs, k, m, d_bm, s) == 0
+            assert L.lab_decode(v, d.data_ptr(), p.data_ptr(), lookups[v].data_ptr(), out.data_ptr(),
+                                S, bs, k, m, sh) == 0
+            torch.cuda.synchronize()
+            if v not in (3, 7, 8) and not torch.equal(d, ref[i]):
+                bad.append(names[v])
+            d.copy_(ref[i])
+    print("incorrect decode variants:", bad, flush=True)
+    b_dec = S * (k // m + 1) * bs
+
+    def run(fn):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.iters)]
+        fn(0)
+        for i in range(args.iters):
+            ev[2 * i].record(s)
+            fn(i + 1)
+            ev[2 * i + 1].record(s)
+        torch.cuda.synchronize()
+        return [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.iters)]
+
+    res = {n: [] for n in names.values()}
+    res["product_decode"] = []
+    res["product_encode"] = []
+    for _ in range(args.rounds):
+        res["product_encode"] += run(lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
+        res["product_decode"] += run(lambda i: xec.decode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m,
+                                                          h_bm, d_bm, s))
+        for v, n in names.items():
+            res[n] += run(lambda i, v=v: L.lab_decode(v, sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(),
+                                                      lookups[v].data_ptr(), out.data_ptr(), S, bs, k, m, sh))
+    for n, ts in sorted(res.items(), key=lambda kv: statistics.median(kv[1])):
+        med = statistics.median(ts)
+        b = S * (k + m) * bs if n == "product_encode" else b_dec
+        print(f"{n:24s} ms_med {med:.4f}  GBps_med {b / (med * 1e-3) / 1e9:.1f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,323 @@
+// lab_kernels.hip -- experimental encode variants (NOT the product).
+//
+// Built into tools/lab/liblab.so by tools/lab/Makefile and driven by
+// tools/lab/lab.py on the GPU box to decide what the product kernel in
+// erasure-code-benchmark_amd/csrc/xec_kernels.hip should become.  Kept in a
+// separate code object so lab instantiations cannot perturb the product's
+// code generation (cdna_hip_programming.md §5.4 rule 19).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// cache-policy aux bits for buffer ops on gfx950: sc0 = 1, nt = 2, sc1 = 16
+constexpr int GLOBAL_NT = -1;  // plain global_load/store with __builtin_nontemporal_*
+
+struct Geo {
+  uint64_t S, bs, k, m, tpb, total;
+};
+
+template <int THREADS>
+__device__ __forceinline__ void decompose(uint64_t t, int order, const Geo& g, uint64_t& c,
+                                          uint64_t& j, uint64_t& chunk) {
+  if (order == 1) {  // stripe fastest
+    c = t % g.S;
+    uint64_t r = t / g.S;
+    j = r % g.m;
+    chunk = r / g.m;
+  } else {  // chunk fastest (product order)
+    chunk = t % g.tpb;
+    uint64_t r = t / g.tpb;
+    j = r % g.m;
+    c = r / g.m;
+  }
+}
+
+template <int NM, int THREADS, int LAUX, int SAUX>
+__device__ __forceinline__ void do_tile(const uint8_t* data, uint8_t* parity, uint64_t c, uint64_t j,
+                                        uint64_t chunk, const Geo& g) {
+  const uint64_t goff = (chunk * THREADS + threadIdx.x) * 16;
+  if (goff >= g.bs) return;
+  const uint8_t* base = data + (c * g.k + j) * g.bs;
+  uint8_t* dst = parity + (c * g.m + j) * g.bs;
+  const uint64_t stride = g.m * g.bs;
+  u32x4 v[NM];
+  if constexpr (LAUX == GLOBAL_NT) {
+#pragma unroll
+    for (int r = 0; r < NM; ++r)
+      v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + r * stride + goff));
+  } else {
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < NM; ++r)
+      v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)goff, (uint32_t)(r * stride), LAUX);
+  }
+  u32x4 acc = v[0];
+#pragma unroll
+  for (int r = 1; r < NM; ++r) acc ^= v[r];
+  if constexpr (SAUX == GLOBAL_NT) {
+    __builtin_nontemporal_store(acc, reinterpret_cast<u32x4*>(dst + goff));
+  } else {
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(acc, ws, (uint32_t)goff, 0, SAUX);
+  }
+}
+
+// order 0: chunk fastest, 1: stripe fastest, 2: chunk fastest with each XCD
+// (blockIdx % 8) given a contiguous range of tiles.
+template <int NM, int THREADS, int ORDER, int LAUX, int SAUX>
+__global__ __launch_bounds__(THREADS) void enc_tile(const uint8_t* data, uint8_t* parity, Geo g) {
+  uint64_t t = blockIdx.x;
+  if (ORDER == 2) {
+    const uint64_t per = (gridDim.x + 7) / 8;
+    t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  if (t >= g.total) return;
+  uint64_t c, j, chunk;
+  decompose<THREADS>(t, ORDER == 1 ? 1 : 0, g, c, j, chunk);
+  do_tile<NM, THREADS, LAUX, SAUX>(data, parity, c, j, chunk, g);
+}
+
+// persistent grid-stride with register double buffering: the next tile's
+// loads are issued before the current tile is reduced and stored.
+template <int NM, int THREADS>
+__global__ __launch_bounds__(THREADS) void enc_persist_db(const uint8_t* data, uint8_t* parity, Geo g) {
+  const uint64_t stride = g.m * g.bs;
+  u32x4 cur[NM], nxt[NM];
+  uint64_t t = blockIdx.x;
+  auto load = [&](uint64_t tt, u32x4* v) {
+    uint64_t c, j, chunk;
+    decompose<THREADS>(tt, 0, g, c, j, chunk);
+    const uint64_t goff = (chunk * THREADS + threadIdx.x) * 16;
+    const uint8_t* base = data + (c * g.k + j) * g.bs;
+#pragma unroll
+    for (int r = 0; r < NM; ++r)
+      v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + r * stride + goff));
+  };
+  if (t >= g.total) return;
+  load(t, cur);
+  for (; t < g.total; t += gridDim.x) {
+    const uint64_t tn = t + gridDim.x;
+    if (tn < g.total) load(tn, nxt);
+    uint64_t c, j, chunk;
+    decompose<THREADS>(t, 0, g, c, j, chunk);
+    const uint64_t goff = (chunk * THREADS + threadIdx.x) * 16;
+    u32x4 acc = cur[0];
+#pragma unroll
+    for (int r = 1; r < NM; ++r) acc ^= cur[r];
+    __builtin_nontemporal_store(acc, reinterpret_cast<u32x4*>(parity + (c * g.m + j) * g.bs + goff));
+#pragma unroll
+    for (int r = 0; r < NM; ++r) cur[r] = nxt[r];
+  }
+}
+
+
+// one-wave tiles of U granules per lane, register budget set by WPE (waves per
+// SIMD the compiler must allow; lower = more VGPRs = more loads in flight)
+template <int NM, int U, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
+void enc_wave(const uint8_t* data, uint8_t* parity, Geo g) {
+  const uint64_t t = blockIdx.x;
+  if (t >= g.total) return;
+  uint64_t c, j, chunk;
+  decompose<64>(t, 0, g, c, j, chunk);
+  const uint64_t off = (chunk * 64 * U + threadIdx.x) * 16;
+  const uint8_t* base = data + (c * g.k + j) * g.bs + off;
+  uint8_t* dst = parity + (c * g.m + j) * g.bs + off;
+  const uint64_t stride = g.m * g.bs;
+  u32x4 v[NM][U];
+#pragma unroll
+  for (int r = 0; r < NM; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[r][u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + r * stride + u * 1024));
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    u32x4 acc = v[0][u];
+#pragma unroll
+    for (int r = 1; r < NM; ++r) acc ^= v[r][u];
+    __builtin_nontemporal_store(acc, reinterpret_cast<u32x4*>(dst + u * 1024));
+  }
+}
+
+
+// ---- decode diagnostics (m = 1, one 1 KiB tile per one-wave workgroup) ----
+// MODE 0: lost member from the bitmap row by lane loads + ballot (product)
+// MODE 1: lost member from a per-stripe u8 table by one scalar load
+// MODE 2: lost member computed as (7c) mod k -- no memory lookup (diagnostic)
+// MODE 3: as 2 but the rebuilt block goes to a separate buffer (diagnostic)
+// MODE 4: as 1 but with grid-stride and the next tile's table entry prefetched
+// MODE 6: as 2, stripe-fastest tile order
+// MODE 7: as 2, rebuilt block written to `out` at the same offset as in data (diagnostic)
+// MODE 8: as 2, rebuilt block written to stripe (c + S/2) % S's lost slot (diagnostic)
+// MODE 9: as 2, store with the default cache policy; MODE 10: store sc1 nt
+template <int NM, int MODE>
+__global__ __launch_bounds__(64) void dec_wave(uint8_t* data, const uint8_t* parity,
+                                               const uint8_t* lookup, uint8_t* out, Geo g) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t stride = g.m * g.bs;
+  for (uint64_t t = blockIdx.x; t < g.total; t += gridDim.x) {
+    uint64_t c, j, chunk;
+    decompose<64>(t, MODE == 6 ? 1 : 0, g, c, j, chunk);
+    int lost;
+    if (MODE == 0) {
+      const uint8_t* row = lookup + c * (g.k + g.m) + j;
+      const bool z = lane < NM && row[(uint64_t)lane * g.m] == 0;
+      const uint64_t mask = __ballot(z);
+      lost = mask ? __builtin_ctzll(mask) : -1;
+    } else if (MODE == 11) {
+      typedef const uint32_t __attribute__((address_space(4))) cu32;
+      const uint64_t rowpos = c * (g.k + g.m) + j;
+      lost = -1;
+#pragma unroll
+      for (int r = NM - 1; r >= 0; --r) {
+        const uint64_t pos = rowpos + (uint64_t)r * g.m;
+        const uint32_t w = *(cu32*)(lookup + (pos & ~3ull));
+        if (((w >> (8 * (pos & 3))) & 0xffu) == 0) lost = r;
+      }
+    } else if (MODE == 1 || MODE == 4) {
+      lost = (int)(int8_t)lookup[c * g.m + j];
+    } else {
+      lost = (int)((7 * c) % g.k);
+    }
+    lost = __builtin_amdgcn_readfirstlane(lost);
+    if (lost < 0) continue;
+    const uint64_t off = (chunk * 64 + lane) * 16;
+    const uint8_t* base = data + (c * g.k + j) * g.bs;
+    const uint8_t* par = parity + (c * g.m + j) * g.bs;
+    u32x4 v[NM];
+#pragma unroll
+    for (int r = 0; r < NM; ++r)
+      v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>((r == lost ? par : base + r * stride) + off));
+    u32x4 acc = v[0];
+#pragma unroll
+    for (int r = 1; r < NM; ++r) acc ^= v[r];
+    uint8_t* dst = data + (c * g.k + j) * g.bs + lost * stride;
+    if (MODE == 3) dst = out + c * g.bs;
+    if (MODE == 7) dst = out + (c * g.k + j) * g.bs + lost * stride;
+    if (MODE == 8) {
+      const uint64_t c2 = (c + g.S / 2) % g.S;
+      dst = data + (c2 * g.k + j) * g.bs + ((7 * c2) % g.k) * stride;
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (uint32_t)off, 0, MODE == 9 ? 0 : (MODE == 10 ? 0x12 : 2));
+  }
+}
+
+namespace {
+template <int THREADS>
+Geo geo(uint64_t S, uint64_t bs, uint64_t k, uint64_t m) {
+  Geo g{S, bs, k, m, 0, 0};
+  g.tpb = (bs / 16 + THREADS - 1) / THREADS;
+  g.total = S * m * g.tpb;
+  return g;
+}
+template <int NM, int THREADS, int ORDER, int LAUX, int SAUX>
+int launch(const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint64_t m, hipStream_t s) {
+  Geo g = geo<THREADS>(S, bs, k, m);
+  uint64_t grid = ORDER == 2 ? (g.total + 7) / 8 * 8 : g.total;
+  enc_tile<NM, THREADS, ORDER, LAUX, SAUX><<<(uint32_t)grid, THREADS, 0, s>>>(
+      static_cast<const uint8_t*>(d), static_cast<uint8_t*>(p), g);
+  return hipGetLastError() == hipSuccess ? 0 : 6;
+}
+template <int NM, int U, int WPE>
+int launch_wave(const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint64_t m, hipStream_t s) {
+  Geo g = geo<64 * U>(S, bs, k, m);
+  enc_wave<NM, U, WPE><<<(uint32_t)g.total, 64, 0, s>>>(static_cast<const uint8_t*>(d),
+                                                       static_cast<uint8_t*>(p), g);
+  return hipGetLastError() == hipSuccess ? 0 : 6;
+}
+template <int MODE>
+int launch_dec(void* d, const void* p, const void* lookup, void* out, uint64_t S, uint64_t bs,
+               uint64_t k, uint64_t m, uint32_t grid, hipStream_t s) {
+  Geo g = geo<64>(S, bs, k, m);
+  dec_wave<16, MODE><<<grid ? grid : (uint32_t)g.total, 64, 0, s>>>(
+      static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(lookup),
+      static_cast<uint8_t*>(out), g);
+  return hipGetLastError() == hipSuccess ? 0 : 6;
+}
+template <int NM, int THREADS>
+int launch_db(const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint64_t m, uint32_t grid,
+              hipStream_t s) {
+  Geo g = geo<THREADS>(S, bs, k, m);
+  enc_persist_db<NM, THREADS><<<grid, THREADS, 0, s>>>(static_cast<const uint8_t*>(d),
+                                                       static_cast<uint8_t*>(p), g);
+  return hipGetLastError() == hipSuccess ? 0 : 6;
+}
+}  // namespace
+
+extern "C" {
+
+const char* lab_variant_name(int v) {
+  static const char* names[] = {
+      "A_glob_nt_256",     "B_buf_nt_nt_256",   "C_buf_ntsc1_nt_256", "D_buf_all_all_256",
+      "E_buf_def_nt_256",  "F_stripe_first_nt", "G_xcd_contig_nt",    "H_glob_nt_512",
+      "I_glob_nt_1024",    "J_glob_nt_64",      "K_persist_db_2048",  "L_persist_db_1024",
+      "M_buf_sc1_nt_256",  "N_persist_db_4096", "O_buf_nt_sc1nt_256", "P_wave_u1_w8",
+      "Q_wave_u1_w7",      "R_wave_u1_w6",      "S_wave_u1_w4",       "T_wave_u2_w4",
+      "U_wave_u2_w5",      "V_wave_u2_w3",      "W_wave_u1_w5"};
+  return (v >= 0 && v < (int)(sizeof names / sizeof *names)) ? names[v] : nullptr;
+}
+
+const char* lab_dec_name(int v) {
+  static const char* names[] = {"d0_ballot", "d1_table", "d2_computed", "d3_computed_sepout",
+                                "d4_table_gs8192", "d5_ballot_gs8192", "d6_stripe_first",
+                                "d7_out_same_offset", "d8_far_stripe", "d9_store_default",
+                                "d10_store_sc1nt", "d11_scalar_lookup"};
+  return (v >= 0 && v < 12) ? names[v] : nullptr;
+}
+
+// Decode diagnostics for k = 16, m = 1.  lookup = bitmap (d0, d5) or u8 table (d1, d4).
+int lab_decode(int v, void* d, const void* p, const void* lookup, void* out, uint64_t S,
+               uint64_t bs, uint64_t k, uint64_t m, hipStream_t s) {
+  if (k != 16 || m != 1) return 3;
+  switch (v) {
+    case 0: return launch_dec<0>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 1: return launch_dec<1>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 2: return launch_dec<2>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 3: return launch_dec<3>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 4: return launch_dec<4>(d, p, lookup, out, S, bs, k, m, 8192, s);
+    case 5: return launch_dec<0>(d, p, lookup, out, S, bs, k, m, 8192, s);
+    case 6: return launch_dec<6>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 7: return launch_dec<7>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 8: return launch_dec<8>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 9: return launch_dec<9>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 10: return launch_dec<10>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 11: return launch_dec<11>(d, p, lookup, out, S, bs, k, m, 0, s);
+  }
+  return 1;
+}
+
+// Encode for k/m == 16 (the benchmark shape).  Returns 0 or 6.
+int lab_encode(int v, const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint64_t m,
+               hipStream_t s) {
+  if (k / m != 16) return 3;
+  switch (v) {
+    case 0: return launch<16, 256, 0, GLOBAL_NT, GLOBAL_NT>(d, p, S, bs, k, m, s);
+    case 1: return launch<16, 256, 0, 2, 2>(d, p, S, bs, k, m, s);
+    case 2: return launch<16, 256, 0, 0x12, 2>(d, p, S, bs, k, m, s);
+    case 3: return launch<16, 256, 0, 0x13, 0x13>(d, p, S, bs, k, m, s);
+    case 4: return launch<16, 256, 0, 0, 2>(d, p, S, bs, k, m, s);
+    case 5: return launch<16, 256, 1, GLOBAL_NT, GLOBAL_NT>(d, p, S, bs, k, m, s);
+    case 6: return launch<16, 256, 2, GLOBAL_NT, GLOBAL_NT>(d, p, S, bs, k, m, s);
+    case 7: return launch<16, 512, 0, GLOBAL_NT, GLOBAL_NT>(d, p, S, bs, k, m, s);
+    case 8: return launch<16, 1024, 0, GLOBAL_NT, GLOBAL_NT>(d, p, S, bs, k, m, s);
+    case 9: return launch<16, 64, 0, GLOBAL_NT, GLOBAL_NT>(d, p, S, bs, k, m, s);
+    case 10: return launch_db<16, 256>(d, p, S, bs, k, m, 2048, s);
+    case 11: return launch_db<16, 256>(d, p, S, bs, k, m, 1024, s);
+    case 12: return launch<16, 256, 0, 0x10, 2>(d, p, S, bs, k, m, s);
+    case 13: return launch_db<16, 256>(d, p, S, bs, k, m, 4096, s);
+    case 14: return launch<16, 256, 0, 2, 0x12>(d, p, S, bs, k, m, s);
+    case 15: return launch_wave<16, 1, 8>(d, p, S, bs, k, m, s);
+    case 16: return launch_wave<16, 1, 7>(d, p, S, bs, k, m, s);
+    case 17: return launch_wave<16, 1, 6>(d, p, S, bs, k, m, s);
+    case 18: return launch_wave<16, 1, 4>(d, p, S, bs, k, m, s);
+    case 19: return launch_wave<16, 2, 4>(d, p, S, bs, k, m, s);
+    case 20: return launch_wave<16, 2, 5>(d, p, S, bs, k, m, s);
+    case 21: return launch_wave<16, 2, 3>(d, p, S, bs, k, m, s);
+    case 22: return launch_wave<16, 1, 5>(d, p, S, bs, k, m, s);
+  }
+  return 1;
+}
+}

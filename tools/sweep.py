@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--workload", default="cfg3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--unroll", default="1,2,4")
+    ap.add_argument("--unroll", default="1,2")
+    ap.add_argument("--threads", default="64,256")
     ap.add_argument("--grid", default="0,2048,4096")
     ap.add_argument("--nt", default="1,2", help="cache policy: 1 nt, 2 default")
     ap.add_argument("--out", default="")
@@ -68,9 +69,11 @@ def main():
         return [ev[i].elapsed_time(ev[i + 1]) for i in range(args.iters)]
 
     variants = {}
-    for u, g, nt in itertools.product(map(int, args.unroll.split(",")), map(int, args.grid.split(",")),
-                                      map(int, args.nt.split(","))):
-        variants[f"u{u}_g{g}_nt{nt}"] = (u, g, nt)
+    for t, u, g, nt in itertools.product(map(int, args.threads.split(",")),
+                                         map(int, args.unroll.split(",")),
+                                         map(int, args.grid.split(",")),
+                                         map(int, args.nt.split(","))):
+        variants[f"t{t}_u{u}_g{g}_nt{nt}"] = (t, u, g, nt)
 
     # references on the same byte volume
     big = sets[0][0]
@@ -82,13 +85,13 @@ def main():
     results["torch_copy"] = {"GBps": []}
     results["torch_xor2"] = {"GBps": []}
     for _ in range(args.rounds):
-        for name, (u, g, nt) in variants.items():
-            assert xec.set_launch(u, g, nt) == 0
+        for name, (t, u, g, nt) in variants.items():
+            assert xec.set_launch(u, g, nt, t) == 0
             results[name]["enc"] += time_it(
                 lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
             results[name]["dec"] += time_it(
                 lambda i: xec.decode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, h_bm, scratch, s))
-        xec.set_launch(0, 0, 0)
+        xec.set_launch(0, 0, 0, 0)
         t = time_it(lambda i: copy_dst.copy_(big))
         results["torch_copy"]["GBps"] += [2 * big.numel() / (x * 1e-3) / 1e9 for x in t]
         t = time_it(lambda i: torch.bitwise_xor(big[:half // 2 * 2][:half], big[half:half * 2],
