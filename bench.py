@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall budget")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL (default); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--no-scatter", action="store_true",
+                    help="skip the N>1 scatter-inclusive measurement (RCCL send/recv)")
     return ap.parse_args()
 
 
@@ -105,6 +109,39 @@ def cpu_baseline(k, m, bs, budget_s):
             "cpu_model": cpu_model}
 
 
+def measure_scatter(torch, dist, xec, S_total, S, start, k, m, bs, stream, enc_ms, reps=3):
+    """Config 5's RCCL leg: the whole batch starts on rank 0 and is scattered
+    (point-to-point send/recv over xGMI, xec/dist.py) before the encode.
+    Link-bound, so reported beside -- never as -- the device-resident value."""
+    from xec import dist as xdist
+    rank = dist.get_rank()
+    full = torch.empty(S_total * k * bs if rank == 0 else 1, dtype=torch.uint8, device="cuda")
+    if rank == 0:
+        assert xec.fill_splitmix64(full, S_total, k * bs, SEED, stream) == 0
+    local = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+    ts = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        xdist.scatter_stripes(full if rank == 0 else None, local, S_total, k * bs)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    t = torch.tensor([min(ts)], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_sc = t.item()
+    ref = torch.empty_like(local)
+    assert xec.fill_splitmix64(ref, S, k * bs, SEED + start, stream) == 0
+    ok = bool(torch.equal(ref, local))
+    del full, local, ref
+    moved = (S_total - (S_total // dist.get_world_size())) * k * bs  # bytes leaving rank 0
+    return {"ok": ok, "scatter_ms": round(t_sc * 1e3, 3),
+            "root_egress_GBps": round(moved / t_sc / 1e9, 1),
+            "scatter_inclusive_encode_GBps_data": round(
+                S_total * k * bs / (t_sc + enc_ms * 1e-3) / 1e9, 1),
+            "note": "batch starts on rank 0; RCCL send/recv of stripe ranges; link-bound"}
+
+
 def main():
     args = parse()
     import torch
@@ -118,12 +155,19 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local)
-    st = xec.init(local)
+    # one process per GPU; the modulo only matters when rehearsing N>1 on
+    # fewer GPUs (device_count() does not initialise the GPU on this image)
+    dev = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
+    st = xec.init(dev)
     if st != xec.Status.SUCCESS:
-        sys.exit(f"xec_init({local}) failed: {st!r}")
+        sys.exit(f"xec_init({dev}) failed: {st!r}")
+    backend = args.dist_backend
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     k, m, bs, S_per, desc = WORKLOADS[args.workload]
     if args.stripes:
@@ -209,8 +253,14 @@ def main():
             ok &= bool(torch.equal(fresh, d))
         del fresh
 
+    scatter = None
+    if world > 1 and backend == "nccl" and not args.no_scatter:
+        scatter = measure_scatter(torch, dist, xec, S_total, S, start, k, m, bs, stream,
+                                  enc_ms)
+        ok &= scatter.pop("ok")
+
     t = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0], dtype=torch.float64,
-                     device="cuda")
+                     device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, enc_ms_max, dec_ms_max, bad = t.tolist()
@@ -259,6 +309,8 @@ def main():
         }
         if traffic_src:
             out["roofline"]["traffic_source"] = traffic_src.get("source")
+        if scatter:
+            out["scatter"] = scatter
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
