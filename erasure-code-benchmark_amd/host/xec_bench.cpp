@@ -4,7 +4,10 @@
 //
 //   xec_bench [-s message_bytes] [-b block_bytes] [-k data] [-m parity]
 //             [-l lost_per_stripe] [-i iterations] [-w warmup] [-t cpu_threads]
-//             [-d device] [-r seed] [-o out.csv] [--no-header]
+//             [-d device] [-r seed] [-o out.csv] [--no-header] [-f sweep_file]
+// -f runs every line "message_bytes block_bytes k m lost" of sweep_file in
+// this process (one CSV row each), like the reference's config cross-product
+// (benchmark_suite.cpp:220-318).
 // Sizes accept K/M/G suffixes (binary).  Defaults: BASELINE.json configs[2]
 // (k=16+1, 1 MiB blocks, 256 stripes = 4 GiB message), 1 lost block, 10
 // iterations, 0 warm-up (the reference's defaults, benchmark_suite.cpp:30-31).
@@ -16,6 +19,7 @@
 #include <fstream>
 #include <iostream>
 #include <string>
+#include <vector>
 
 #include "runner.hpp"
 #include "xorec_hip_bm.hpp"
@@ -38,7 +42,7 @@ void usage() {
   std::fprintf(stderr,
                "usage: xec_bench [-s message_bytes] [-b block_bytes] [-k data] [-m parity]\n"
                "                 [-l lost] [-i iters] [-w warmup] [-t threads] [-d device]\n"
-               "                 [-r seed] [-o out.csv] [--no-header]\n");
+               "                 [-r seed] [-o out.csv] [--no-header] [-f sweep_file]\n");
 }
 
 }  // namespace
@@ -50,7 +54,7 @@ int main(int argc, char** argv) {
   cfg.message_size = 256ull * 16 * (1 << 20);
   cfg.num_lost_blocks = 1;
   cfg.num_cpu_threads = static_cast<size_t>(omp_get_max_threads());
-  std::string out;
+  std::string out, sweep;
   bool header = true;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -70,18 +74,42 @@ int main(int argc, char** argv) {
     else if (a == "-r") cfg.seed = parse_size(val());
     else if (a == "-o") out = val();
     else if (a == "--no-header") header = false;
+    else if (a == "-f") sweep = val();
     else if (a == "-h" || a == "--help") { usage(); return 0; }
     else { usage(); return 2; }
   }
-  cfg.ec_params = {k + m, k};
-  if (cfg.num_lost_blocks > m) {
-    // the reference prints and exits (utils.cpp:102-105)
-    std::fprintf(stderr, "lost blocks per stripe (%zu) must be <= parity blocks (%zu)\n",
-                 cfg.num_lost_blocks, m);
-    return 2;
+  std::vector<xec::BenchmarkConfig> cfgs;
+  if (sweep.empty()) {
+    cfg.ec_params = {k + m, k};
+    cfgs.push_back(cfg);
+  } else {
+    std::ifstream in(sweep);
+    if (!in) {
+      std::fprintf(stderr, "cannot open %s\n", sweep.c_str());
+      return 2;
+    }
+    std::string line;
+    while (std::getline(in, line)) {
+      if (line.empty() || line[0] == '#') continue;
+      unsigned long long ms, b, kk, mm, l;
+      if (std::sscanf(line.c_str(), "%llu %llu %llu %llu %llu", &ms, &b, &kk, &mm, &l) != 5) continue;
+      xec::BenchmarkConfig c = cfg;
+      c.message_size = ms;
+      c.block_size = b;
+      c.ec_params = {kk + mm, kk};
+      c.num_lost_blocks = l;
+      cfgs.push_back(c);
+    }
+  }
+  for (const auto& c : cfgs) {
+    if (c.num_lost_blocks > xec::parity_blocks(c)) {
+      // the reference prints and exits (utils.cpp:102-105)
+      std::fprintf(stderr, "lost blocks per stripe (%zu) must be <= parity blocks (%zu)\n",
+                   c.num_lost_blocks, xec::parity_blocks(c));
+      return 2;
+    }
   }
   try {
-    xec::RunResult r = xec::run_generic<xec::XorecBenchmarkHip>("XOR-EC (HIP gfx950)", cfg);
     std::ofstream f;
     std::ostream* os = &std::cout;
     if (!out.empty()) {
@@ -89,8 +117,14 @@ int main(int argc, char** argv) {
       os = &f;
     }
     if (header) xec::write_csv_header(*os);
-    xec::write_csv_row(*os, r, cfg);
-    return r.err_msg.empty() ? 0 : 1;
+    int rc = 0;
+    for (const auto& c : cfgs) {
+      xec::RunResult r = xec::run_generic<xec::XorecBenchmarkHip>("XOR-EC (HIP gfx950)", c);
+      xec::write_csv_row(*os, r, c);
+      os->flush();
+      if (!r.err_msg.empty()) rc = 1;
+    }
+    return rc;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "xec_bench: %s\n", e.what());
     return 3;
