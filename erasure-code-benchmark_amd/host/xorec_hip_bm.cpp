@@ -23,6 +23,12 @@ void check_hip(hipError_t e, const char* what) {
 XorecBenchmarkHip::XorecBenchmarkHip(const BenchmarkConfig& config)
     : AbstractBenchmark(config), m_seed(config.seed) {
   if (xec_init(config.device_id) != XEC_SUCCESS) throw std::runtime_error("xec_init failed");
+  if (config.sync_mode > 0) {
+    static const unsigned flags[] = {0, hipDeviceScheduleSpin, hipDeviceScheduleYield,
+                                     hipDeviceScheduleBlockingSync};
+    // only possible before the device's context is active; ignored otherwise
+    (void)hipSetDeviceFlags(flags[config.sync_mode & 3]);
+  }
   check_hip(hipStreamCreateWithFlags(&m_stream, hipStreamNonBlocking), "hipStreamCreate");
   const size_t S = m_chunks;
   const size_t data_bytes = std::max<size_t>(S * m_chunk_data_size, 64);
