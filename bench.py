@@ -84,7 +84,7 @@ def cpu_baseline(k, m, bs, budget_s):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     threads = min(threads, os.cpu_count() or threads)
     o = xo.COracle()
-    S = 64  # 64 stripes x 16 x 1 MiB = 1 GiB data: beyond any host LLC
+    S = max(1, (1 << 30) // (k * bs))  # ~1 GiB of data: beyond any host LLC
     data, parity = o.batch(S, k, m, bs, threads=threads)
     bm = xo.single_erasure_bitmap(S, k, m)
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)

@@ -176,6 +176,27 @@ xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint6
              : XEC_DEVICE_ERROR;
 }
 
+xec_status xec_write_validation_pattern(void* d_data, size_t nblocks, size_t bs, uint64_t seed,
+                                        hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  if (bs < 2) return XEC_INVALID_SIZE;
+  if (bs >= 16 && bs % 16 == 0 && reinterpret_cast<uintptr_t>(d_data) % 16 != 0)
+    return XEC_INVALID_ALIGNMENT;
+  return xec::launch_pattern(d_data, nblocks, bs, seed, stream) == hipSuccess ? XEC_SUCCESS
+                                                                              : XEC_DEVICE_ERROR;
+}
+
+xec_status xec_validate_blocks(const void* d_data, size_t nblocks, size_t bs, uint32_t* d_bad,
+                               hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  if (bs >= 16 && bs % 16 == 0 && reinterpret_cast<uintptr_t>(d_data) % 16 != 0)
+    return XEC_INVALID_ALIGNMENT;
+  if (reinterpret_cast<uintptr_t>(d_bad) % 4 != 0) return XEC_INVALID_ALIGNMENT;
+  return xec::launch_validate(d_data, nblocks, bs, d_bad, stream) == hipSuccess
+             ? XEC_SUCCESS
+             : XEC_DEVICE_ERROR;
+}
+
 xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_threads) {
   if (unroll != 0 && unroll != 1 && unroll != 2) return XEC_INVALID_SIZE;
   if (max_grid < 0 || cache_policy < 0 || cache_policy > 2) return XEC_INVALID_SIZE;

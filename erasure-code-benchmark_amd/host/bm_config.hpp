@@ -28,6 +28,9 @@ struct BenchmarkConfig {
   size_t threads_per_gpu_block = 256; // CSV only
   int device_id = 0;            // new: HIP device of this process
   uint64_t seed = 0;            // new: explicit seed (reference seeds from the clock)
+  bool host_validation = false; // new: true = payload written/checked on the host and copied
+                                //   (the reference's way, xorec_gpu_cmp_bm.cpp:25-37,91-104);
+                                //   false = on the device (xec_write_validation_pattern)
   int sync_mode = 0;            // new: 0 runtime default, 1 spin, 2 yield, 3 blocking sync
                                 // (hipSetDeviceFlags; CUDA's default "auto" spins when
                                 // contexts < cores, which is what the reference ran under)

@@ -6,6 +6,7 @@
 //             [-l lost_per_stripe] [-i iterations] [-w warmup] [-t cpu_threads]
 //             [-d device] [-r seed] [-o out.csv] [--no-header] [-f sweep_file]
 //             [-y sync_mode: 0 default, 1 spin, 2 yield, 3 blocking]
+//             [-V: validation payload on the host + copies, as the reference]
 // -f runs every line "message_bytes block_bytes k m lost" of sweep_file in
 // this process (one CSV row each), like the reference's config cross-product
 // (benchmark_suite.cpp:220-318).
@@ -44,7 +45,7 @@ void usage() {
                "usage: xec_bench [-s message_bytes] [-b block_bytes] [-k data] [-m parity]\n"
                "                 [-l lost] [-i iters] [-w warmup] [-t threads] [-d device]\n"
                "                 [-r seed] [-o out.csv] [--no-header] [-f sweep_file]\n"
-               "                 [-y sync_mode]\n");
+               "                 [-y sync_mode] [-V]\n");
 }
 
 }  // namespace
@@ -78,6 +79,7 @@ int main(int argc, char** argv) {
     else if (a == "--no-header") header = false;
     else if (a == "-f") sweep = val();
     else if (a == "-y") cfg.sync_mode = std::atoi(val());
+    else if (a == "-V") cfg.host_validation = true;
     else if (a == "-h" || a == "--help") { usage(); return 0; }
     else { usage(); return 2; }
   }

@@ -21,7 +21,7 @@ void check_hip(hipError_t e, const char* what) {
 }  // namespace
 
 XorecBenchmarkHip::XorecBenchmarkHip(const BenchmarkConfig& config)
-    : AbstractBenchmark(config), m_seed(config.seed) {
+    : AbstractBenchmark(config), m_host_validation(config.host_validation), m_seed(config.seed) {
   if (xec_init(config.device_id) != XEC_SUCCESS) throw std::runtime_error("xec_init failed");
   if (config.sync_mode > 0) {
     static const unsigned flags[] = {0, hipDeviceScheduleSpin, hipDeviceScheduleYield,
@@ -39,7 +39,9 @@ XorecBenchmarkHip::XorecBenchmarkHip(const BenchmarkConfig& config)
   check_hip(hipMalloc(&m_d_bitmap, bitmap_bytes), "hipMalloc bitmap");
   check_hip(hipMalloc(&m_d_erase, bitmap_bytes), "hipMalloc erase bitmap");
   check_hip(hipHostMalloc(&m_h_bitmap, bitmap_bytes, hipHostMallocDefault), "hipHostMalloc bitmap");
-  check_hip(hipHostMalloc(&m_h_stage, data_bytes, hipHostMallocDefault), "hipHostMalloc stage");
+  check_hip(hipMalloc(&m_d_bad, sizeof(uint32_t)), "hipMalloc bad counter");
+  if (m_host_validation)
+    check_hip(hipHostMalloc(&m_h_stage, data_bytes, hipHostMallocDefault), "hipHostMalloc stage");
 }
 
 XorecBenchmarkHip::~XorecBenchmarkHip() noexcept {
@@ -49,7 +51,8 @@ XorecBenchmarkHip::~XorecBenchmarkHip() noexcept {
   (void)hipFree(m_d_bitmap);
   (void)hipFree(m_d_erase);
   (void)hipHostFree(m_h_bitmap);
-  (void)hipHostFree(m_h_stage);
+  (void)hipFree(m_d_bad);
+  if (m_h_stage) (void)hipHostFree(m_h_stage);
   if (m_stream) (void)hipStreamDestroy(m_stream);
 }
 
@@ -65,6 +68,12 @@ void XorecBenchmarkHip::setup() noexcept {
 void XorecBenchmarkHip::write_data_buffer() noexcept {
   const long nblocks = static_cast<long>(m_chunks * m_chunk_data_blocks);
   const uint64_t base = m_seed + (m_round << 32);
+  if (!m_host_validation) {
+    (void)xec_write_validation_pattern(m_data, static_cast<size_t>(nblocks), m_block_size, base,
+                                       m_stream);
+    (void)hipStreamSynchronize(m_stream);
+    return;
+  }
   omp_set_num_threads(static_cast<int>(std::max<size_t>(m_threads, 1)));
 #pragma omp parallel for schedule(static)
   for (long b = 0; b < nblocks; ++b)
@@ -108,6 +117,15 @@ void XorecBenchmarkHip::simulate_data_loss() noexcept {
 // XorecBenchmarkGpuCmp::check_for_corruption (xorec_gpu_cmp_bm.cpp:91-104):
 // copy the data back and validate every data block's embedded checksum.
 bool XorecBenchmarkHip::check_for_corruption() const noexcept {
+  if (!m_host_validation) {
+    uint32_t bad = 1;
+    if (xec_validate_blocks(m_data, m_chunks * m_chunk_data_blocks, m_block_size, m_d_bad,
+                            m_stream) != XEC_SUCCESS ||
+        hipMemcpyAsync(&bad, m_d_bad, sizeof bad, hipMemcpyDeviceToHost, m_stream) != hipSuccess ||
+        hipStreamSynchronize(m_stream) != hipSuccess)
+      return false;
+    return bad == 0;
+  }
   if (hipMemcpyAsync(m_h_stage, m_data, m_chunks * m_chunk_data_size, hipMemcpyDeviceToHost,
                      m_stream) != hipSuccess)
     return false;

@@ -10,7 +10,9 @@
 //     (xorec_gpu_cmp_bm.cpp:71-89);
 //   - parity is not destroyed by decode, so check_for_corruption may also
 //     re-verify parity (it checks data blocks, as the reference does);
-//   - seeds are explicit (config.seed), so every run is reproducible.
+//   - seeds are explicit (config.seed), so every run is reproducible;
+//   - the validation payload is written and checked on the device by default
+//     (config.host_validation = true restores the host + copy path).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -48,7 +50,9 @@ class XorecBenchmarkHip : public AbstractBenchmark {
   uint8_t* m_d_bitmap = nullptr;    // device scratch, S*(k+m)
   uint8_t* m_d_erase = nullptr;     // device copy of the erasure bitmap
   uint8_t* m_h_bitmap = nullptr;    // pinned host, S*(k+m)
-  uint8_t* m_h_stage = nullptr;     // pinned host staging for data in/out
+  uint8_t* m_h_stage = nullptr;     // pinned host staging (host_validation only)
+  uint32_t* m_d_bad = nullptr;      // device counter of corrupted blocks
+  bool m_host_validation;
   uint64_t m_seed;
   uint64_t m_round = 0;             // bumps per setup(): fresh payload per iteration
   int m_last_status = 0;

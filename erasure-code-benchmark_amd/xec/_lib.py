@@ -24,7 +24,7 @@ EXPORTED = (
     "xec_init", "xec_encode", "xec_decode", "xec_check_bitmap", "xec_check_args",
     "xec_erase", "xec_fill_splitmix64", "xec_set_launch", "xec_status_string",
     "xec_build_info", "xec_pipeline_create", "xec_pipeline_destroy", "xec_pipeline_encode",
-    "xec_pipeline_decode",
+    "xec_pipeline_decode", "xec_write_validation_pattern", "xec_validate_blocks",
 )
 
 
@@ -83,6 +83,8 @@ def lib() -> ctypes.CDLL:
         "xec_pipeline_destroy": ([vp], st),
         "xec_pipeline_encode": ([vp, vp, vp, sz], st),
         "xec_pipeline_decode": ([vp, vp, vp, sz, vp], st),
+        "xec_write_validation_pattern": ([vp, sz, sz, ctypes.c_uint64, vp], st),
+        "xec_validate_blocks": ([vp, sz, sz, vp, vp], st),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

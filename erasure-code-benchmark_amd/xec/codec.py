@@ -59,6 +59,18 @@ def fill_splitmix64(d_buf, S: int, stripe_bytes: int, seed_base: int, stream=Non
                                             _stream(stream)))
 
 
+def write_validation_pattern(d_data, nblocks: int, bs: int, seed: int, stream=None) -> Status:
+    """xec_write_validation_pattern -- utils.cpp:35-69 on the device."""
+    return Status(lib().xec_write_validation_pattern(_ptr(d_data), nblocks, bs, seed,
+                                                     _stream(stream)))
+
+
+def validate_blocks(d_data, nblocks: int, bs: int, d_bad, stream=None) -> Status:
+    """xec_validate_blocks -- utils.cpp:72-97 on the device; *d_bad = failing blocks."""
+    return Status(lib().xec_validate_blocks(_ptr(d_data), nblocks, bs, _ptr(d_bad),
+                                            _stream(stream)))
+
+
 def check_bitmap(h_bitmap, S: int, k: int, m: int) -> tuple[Status, bool]:
     """Host-only recoverability scan; returns (status, needs_recovery)."""
     needs = ctypes.c_int(0)

@@ -103,6 +103,19 @@ xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k
 xec_status xec_fill_splitmix64(void* d_buf, size_t S, size_t stripe_bytes, uint64_t seed_base,
                                hipStream_t stream);
 
+/* Device-side validation payload: the reference's
+ * write_validation_pattern / validate_block (src/utils/utils.cpp:35-97) run on
+ * the GPU over nblocks consecutive blocks of bs bytes.  Block b gets PCG32
+ * bytes from offset 8 (state RANDOM_SEED + seed + b, stream 1 -- an explicit
+ * seed instead of the reference's wall clock), its length at 4 and the
+ * rotate-add checksum at 0; blocks under 16 bytes are one repeated byte.
+ * xec_validate_blocks writes the number of blocks failing the check to *d_bad
+ * (device memory).  16-byte alignment is required when bs % 16 == 0. */
+xec_status xec_write_validation_pattern(void* d_data, size_t nblocks, size_t bs, uint64_t seed,
+                                        hipStream_t stream);
+xec_status xec_validate_blocks(const void* d_data, size_t nblocks, size_t bs, uint32_t* d_bad,
+                               hipStream_t stream);
+
 /* Launch-shape override for tuning sweeps (process-wide, not thread-safe
  * against concurrent launches).  Each argument 0 = the measured default:
  *   unroll        16-byte granules per lane per class member: 1 or 2;

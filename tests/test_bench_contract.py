@@ -1,0 +1,44 @@
+"""bench.py keeps the driver's contract: one JSON line with the required keys,
+roofline + cpu_baseline objects, verified results (GPU, small sizes)."""
+from __future__ import annotations
+
+import json
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+            "roofline", "cpu_baseline"}
+
+
+def run_bench(*args):
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True,
+                       text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("workload,stripes", [("cfg3", 16), ("cfg2", 64), ("cfg4", 512)])
+def test_bench_json_line(workload, stripes):
+    out = run_bench("--workload", workload, "--stripes", str(stripes), "--steps", "3",
+                    "--warmup", "1", "--cpu-seconds", "0.5")
+    assert REQUIRED <= set(out)
+    assert out["verified"] is True
+    assert out["n_gpus"] == 1 and out["steps"] == 3 and out["warmup"] == 1
+    assert out["unit"] == "GB/s" and out["higher_is_better"] is True
+    assert out["scaling"] == "weak" and out["dtype"] == "u8"
+    assert out["config"]["workload"].startswith(workload)
+    r = out["roofline"]
+    assert r["bound"] == "hbm" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    c = out["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
+    assert out["value"] > 0

@@ -36,6 +36,7 @@ def test_cli_help_and_lost_check():
     ("-s", "8M", "-b", "1K", "-k", "32", "-m", "8", "-l", "0", "-i", "3"),
     ("-s", "32M", "-b", "4K", "-k", "16", "-m", "4", "-l", "2", "-i", "3"),
     ("-s", "1G", "-b", "1M", "-k", "16", "-m", "1", "-l", "1", "-i", "2", "-w", "1"),
+    ("-s", "64M", "-b", "8K", "-k", "16", "-m", "4", "-l", "3", "-i", "2", "-V"),
 ])
 def test_harness_rows_clean(args):
     r = run(*args, "-r", "7")

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--gap-ms", type=float, default=0.0, help="host sleep between launches")
     ap.add_argument("--out", default="")
     ap.add_argument("--decode", action="store_true", help="time the decode diagnostics")
+    ap.add_argument("--ceiling", action="store_true", help="time read/write/copy ceilings")
     args = ap.parse_args()
 
     import torch
@@ -64,6 +65,8 @@ def main():
 
     if args.decode:
         return decode_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh)
+    if args.ceiling:
+        return ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh)
 
     # correctness of every variant first
     bad = []
@@ -167,6 +170,34 @@ def decode_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):
         med = statistics.median(ts)
         b = S * (k + m) * bs if n == "product_encode" else b_dec
         print(f"{n:24s} ms_med {med:.4f}  GBps_med {b / (med * 1e-3) / 1e9:.1f}")
+
+
+
+def ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):
+    L.lab_ceiling.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
+
+    def run(fn):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.iters)]
+        fn(0)
+        for i in range(args.iters):
+            ev[2 * i].record(s)
+            fn(i + 1)
+            ev[2 * i + 1].record(s)
+        torch.cuda.synchronize()
+        return [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.iters)]
+
+    bytes_ = {"read_only_16way": S * k * bs, "write_only": S * bs, "copy": 2 * S * bs,
+              "product_encode": S * (k + m) * bs}
+    res = {n: [] for n in bytes_}
+    for _ in range(args.rounds):
+        res["product_encode"] += run(lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
+        for mode, n in enumerate(["read_only_16way", "write_only", "copy"]):
+            res[n] += run(lambda i, mode=mode: L.lab_ceiling(mode, sets[i % 2][0].data_ptr(),
+                                                              sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
+    for n, ts in res.items():
+        med = statistics.median(ts)
+        print(f"{n:20s} ms_med {med:.4f}  GBps_med {bytes_[n] / (med * 1e-3) / 1e9:.1f}  "
+              f"GBps_best {bytes_[n] / (min(ts) * 1e-3) / 1e9:.1f}")
 
 
 if __name__ == "__main__":
