@@ -75,16 +75,64 @@ def load_traffic(workload):
     return t.get("encode_hbm_bytes_per_launch"), t
 
 
+def _cpu_model():
+    model, avx512 = "", False
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name") and not model:
+                model = line.split(":", 1)[1].strip()
+            if line.startswith("flags"):
+                avx512 = " avx512f" in line
+                break
+    except OSError:
+        pass
+    return model, avx512
+
+
+def cpu_baseline_reference(k, m, bs, budget_s, threads, S):
+    """The reference's own CPU XOR-EC (src/xorec/xorec.cpp, compiled unmodified
+    into oracle/_ref/ref_driver by oracle/Makefile in the build container), run
+    in the CPU plugin's loop (xorec_bm.cpp:27-58: OpenMP over stripes)."""
+    import subprocess
+    drv = ROOT / "oracle" / "_ref" / "ref_driver"
+    if not drv.exists():
+        return None
+    model, avx512 = _cpu_model()
+    version = 3 if avx512 else 2  # XorecVersion AVX512 / AVX2 (xorec_utils.hpp:38-43)
+    try:
+        p = subprocess.run([str(drv), "bench", str(k), str(m), str(bs), str(S), str(version),
+                            str(threads), str(budget_s)], capture_output=True, text=True,
+                           timeout=budget_s * 4 + 120)
+        r = dict(line.split(" ", 1) for line in p.stdout.strip().splitlines())
+        if p.returncode != 0 or int(r["fail"]) != 0:
+            return None
+        reps, t = int(r["reps"]), float(r["seconds"])
+    except Exception:  # noqa: BLE001 - fall back to the restatement
+        return None
+    b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
+    return {"value": round(reps * (b_enc + b_dec) / t / 1e9, 2), "unit": "GB/s",
+            "cores": threads, "kind": "reference",
+            "sample": f"{reps} x (encode+decode) of {S} stripes k={k}+{m} {bs >> 10} KiB, "
+                      f"reference src/xorec xorec_encode/xorec_decode "
+                      f"(XorecVersion {'AVX512' if version == 3 else 'AVX2'}), OpenMP over "
+                      f"stripes as xorec_bm.cpp:30, {t:.1f} s wall",
+            "cpu_model": model}
+
+
 def cpu_baseline(k, m, bs, budget_s):
-    """Oracle restatement of the reference CPU path (xorec_bm.cpp:27-58, OpenMP
-    over stripes) timed on this host on a bounded sample of the same workload."""
+    """The reference CPU path (xorec_bm.cpp:27-58, OpenMP over stripes) timed on
+    this host on a bounded sample of the same workload: the reference's own code
+    when oracle/_ref was built, else the oracle's C restatement ("port")."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    S = max(1, (1 << 30) // (k * bs))  # ~1 GiB of data: beyond any host LLC
+    ref = cpu_baseline_reference(k, m, bs, budget_s, threads, S)
+    if ref is not None:
+        return ref
     sys.path.insert(0, str(ROOT / "oracle"))
     import xorec_oracle as xo  # the CPU baseline leg is the only bench use of oracle/
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
     o = xo.COracle()
-    S = max(1, (1 << 30) // (k * bs))  # ~1 GiB of data: beyond any host LLC
     data, parity = o.batch(S, k, m, bs, threads=threads)
     bm = xo.single_erasure_bitmap(S, k, m)
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
@@ -95,14 +143,7 @@ def cpu_baseline(k, m, bs, budget_s):
         assert o.decode_batch(data, parity, S, bs, k, m, bm, threads) == 0
         t_tot += time.perf_counter() - t0
         reps += 1
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    cpu_model = _cpu_model()[0]
     return {"value": round(reps * (b_enc + b_dec) / t_tot / 1e9, 2), "unit": "GB/s",
             "cores": threads, "kind": "port",
             "sample": f"{reps} x (encode+decode) of {S} stripes k={k}+{m} {bs >> 10} KiB "

@@ -15,8 +15,12 @@
 //   dec K M BS S SEED VERSION MODE [ARG]     MODE: single7 | pattern FILE | none
 //   chk K M BS DATA_MISALIGN PARITY_MISALIGN
 //   val BS FILE                               validate_block per BS-byte block
+//   bench K M BS S VERSION THREADS SECONDS    time the reference CPU path (bench.py's
+//                                             cpu_baseline, kind "reference")
 #include "xorec.hpp"
 #include "utils.hpp"
+
+#include <omp.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -128,6 +132,42 @@ int main(int argc, char** argv) {
     XorecResult e = xorec_encode(data + dm, parity + pm, bs, k, m, XorecVersion::Scalar);
     XorecResult d = xorec_decode(data + dm, parity + pm, bs, k, m, bitmap.data(), XorecVersion::Scalar);
     std::printf("encode %d\ndecode %d\n", static_cast<int>(e), static_cast<int>(d));
+    return 0;
+  }
+
+  if (cmd == "bench") {
+    // bench K M BS S VERSION THREADS SECONDS: the reference's CPU plugin loop
+    // (XorecBenchmark::encode/decode, xorec_bm.cpp:27-58: omp parallel for
+    // over stripes calling xorec_encode / xorec_decode), timed on the
+    // reference's own xorec code; single erasure (7c) mod k per stripe.
+    size_t k = std::strtoull(argv[2], nullptr, 0), m = std::strtoull(argv[3], nullptr, 0);
+    size_t bs = std::strtoull(argv[4], nullptr, 0), S = std::strtoull(argv[5], nullptr, 0);
+    int v = std::atoi(argv[6]), threads = std::atoi(argv[7]);
+    double budget = std::atof(argv[8]);
+    omp_set_num_threads(threads);
+    uint8_t* data = alloc64(S * k * bs);
+    uint8_t* parity = alloc64(S * m * bs);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < (long)S; ++c) fill(data + c * k * bs, 1, k * bs, 1896 + c);
+    std::vector<uint8_t> bitmap(S * (k + m), 1);
+    for (size_t c = 0; c < S; ++c) bitmap[c * (k + m) + (7 * c) % k] = 0;
+    int fail = 0, reps = 0;
+    double t = 0;
+    while (t < budget && reps < 100000) {
+      double t0 = omp_get_wtime();
+#pragma omp parallel for schedule(static) reduction(+ : fail)
+      for (long c = 0; c < (long)S; ++c)
+        fail += xorec_encode(data + c * k * bs, parity + c * m * bs, bs, k, m, ver(v)) !=
+                XorecResult::Success;
+#pragma omp parallel for schedule(static) reduction(+ : fail)
+      for (long c = 0; c < (long)S; ++c)
+        fail += xorec_decode(data + c * k * bs, parity + c * m * bs, bs, k, m,
+                             bitmap.data() + c * (k + m), ver(v)) != XorecResult::Success;
+      t += omp_get_wtime() - t0;
+      ++reps;
+    }
+    std::printf("reps %d\nseconds %.6f\nfail %d\nparity_fnv %016llx\n", reps, t, fail,
+                (unsigned long long)fnv(parity, S * m * bs));
     return 0;
   }
 
