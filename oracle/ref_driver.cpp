@@ -21,6 +21,7 @@
 #include "utils.hpp"
 
 #include <omp.h>
+#include <sys/mman.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -42,9 +43,16 @@ uint64_t fnv(const uint8_t* p, size_t n, uint64_t h = 0xcbf29ce484222325ull) {
   return h;
 }
 
+// 64-B aligned (the reference's ALIGNMENT, utils.hpp:25).  With REF_HUGEPAGES=1
+// the buffer is 2 MiB aligned and madvise(MADV_HUGEPAGE)d, as numpy does for the
+// oracle's buffers, so both CPU baselines see the same page size.
 uint8_t* alloc64(size_t n) {
-  size_t r = (n + 63) / 64 * 64 + 64;
-  auto* p = static_cast<uint8_t*>(std::aligned_alloc(64, r));
+  const char* hp = std::getenv("REF_HUGEPAGES");
+  const bool huge = hp && hp[0] == '1' && n >= (4u << 20);
+  const size_t align = huge ? (2u << 20) : 64;
+  size_t r = (n + align - 1) / align * align + align;
+  auto* p = static_cast<uint8_t*>(std::aligned_alloc(align, r));
+  if (huge) madvise(p, r, MADV_HUGEPAGE);
   std::memset(p, 0, r);
   return p;
 }
