@@ -94,9 +94,13 @@ __device__ __forceinline__ void xor_members(const uint8_t* base, uint64_t stride
   if constexpr (NM > 0) {
     if (off + (U - 1) * kStep < bs) {  // whole tile inside the block: no predication
       u32x4 v[NM][U];
+      // A running lane pointer (one 64-bit VGPR add per member) instead of NM
+      // uniform member addresses, which the compiler would park in SGPRs.
+      const uint8_t* p = base + off;
+      const uint8_t* ps = sub + off;
 #pragma unroll
-      for (int r = 0; r < NM; ++r) {
-        const uint8_t* src = (r == subst ? sub : base + (uint64_t)r * stride) + off;
+      for (int r = 0; r < NM; ++r, p += stride) {
+        const uint8_t* src = r == subst ? ps : p;
 #pragma unroll
         for (int u = 0; u < U; ++u) v[r][u] = ld16<NT>(src + u * kStep);
       }
@@ -150,55 +154,46 @@ __global__ __launch_bounds__(T) void encode_kernel(const uint8_t* __restrict__ d
 }
 
 // ---------------------------------------------------------------------------
-// decode: for the (at most one, checked on the host) lost data block L of
-// class j: data[c][L] = parity[c][j] ^ XOR_{r != L} data[c][j + r*m]
-//                                                            (xorec.cpp:79-108)
-// The lost member is found from the class's bitmap bytes with scalar loads
-// (compiled member counts) or one byte load per lane and a wave ballot
-// (runtime member counts); every wave does this itself (no LDS, no barrier).
-// The scalar path reads the aligned dword containing each byte: it cannot
-// cross a page, so it never faults past the end of the caller's scratch.
+// decode: every lost data block L (at most one per class, checked on the
+// host) of class j = L % m is rebuilt as
+//   data[c][L] = parity[c][j] ^ XOR_{r != L/m} data[c][j + r*m]  (xorec.cpp:79-108)
+// A tile is (stripe c, column chunk) -- not per class -- so a workgroup only
+// exists where there may be work: it scans the stripe's k data bitmap bytes
+// with scalar loads (s_load_dword through the scalar cache; 4 bytes per load,
+// exact zero-byte test in SALU) and rebuilds each lost block it finds.  With
+// one erasure per stripe and m > 1 this launches m times fewer workgroups than
+// a per-class tiling, of which m-1 in m would only have found nothing to do.
+// Absolute addresses are used for the dword loads: the caller's scratch
+// pointer need not be aligned, and an aligned dword never crosses a page.
 // ---------------------------------------------------------------------------
 template <int NM, int U, bool NT, int T>
 __global__ __launch_bounds__(T) void decode_kernel(uint8_t* data, const uint8_t* __restrict__ parity,
                                                    const uint8_t* __restrict__ bitmap, Geometry g) {
   const uint32_t nm = NM > 0 ? (uint32_t)NM : (uint32_t)g.nm;
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t m = (uint32_t)g.m;
+  const uint64_t stride = g.m * g.bs;
   for (uint64_t t = blockIdx.x; t < g.total_tiles; t += gridDim.x) {
-    const TileCoord tc = tile_coord(t, g);
-    const uint8_t* row = bitmap + tc.c * (g.k + g.m) + tc.j;
-    int lost = -1;
-    if constexpr (NM > 0) {
-      // Scalar path: the class's bitmap bytes come through the scalar cache
-      // (one s_load_dword each, issued back to back), no vector round trip
-      // before the data loads can start (measured +3 % over the ballot).
-      // Absolute addresses: the caller's scratch pointer need not be aligned.
-      const uint64_t rowaddr = reinterpret_cast<uint64_t>(row);
-#pragma unroll
-      for (int r = NM - 1; r >= 0; --r) {
-        const uint64_t a = rowaddr + (uint64_t)r * g.m;
-        const uint32_t w = *(const_u32_as4)(a & ~3ull);
-        if (((w >> (8 * (a & 3))) & 0xffu) == 0) lost = r;
-      }
-    } else {
-      for (uint32_t b = 0; b < nm; b += 64) {
-        const uint32_t r = b + lane;
-        const bool z = (r < nm) && (row[(uint64_t)r * g.m] == 0);
-        const uint64_t mask = __ballot(z);
-        if (mask) {
-          lost = (int)(b + (uint32_t)__builtin_ctzll(mask));
-          break;
-        }
+    const uint64_t chunk = t % g.tiles_per_block;
+    const uint64_t c = t / g.tiles_per_block;
+    const uint64_t rowaddr = reinterpret_cast<uint64_t>(bitmap + c * (g.k + g.m));
+    const uint64_t end = rowaddr + g.k;
+    uint8_t* sdata = data + c * g.k * g.bs;
+    const uint8_t* spar = parity + c * g.m * g.bs;
+    const uint64_t off = (chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+    for (uint64_t a = rowaddr & ~3ull; a < end; a += 4) {
+      const uint32_t w = *(const_u32_as4)a;
+      uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;  // zero bytes
+      if (a < rowaddr) z &= 0xFFFFFFFFu << (8 * (uint32_t)(rowaddr - a));
+      if (a + 4 > end) z &= 0xFFFFFFFFu >> (8 * (uint32_t)(a + 4 - end));
+      while (z) {
+        const uint32_t i = (uint32_t)(a - rowaddr) + ((uint32_t)__builtin_ctz(z) >> 3);
+        z &= z - 1;
+        const uint32_t j = i % m, r = i / m;  // class and member of lost block i
+        uint8_t* base = sdata + (uint64_t)j * g.bs;
+        xor_members<NM, U, NT, T>(base, stride, spar + (uint64_t)j * g.bs, (int)r,
+                                  base + (uint64_t)r * stride, off, g.bs, nm);
       }
     }
-    lost = __builtin_amdgcn_readfirstlane(lost);
-    if (lost < 0) continue;
-    uint8_t* base = data + (tc.c * g.k + tc.j) * g.bs;
-    const uint64_t stride = g.m * g.bs;
-    const uint8_t* par = parity + (tc.c * g.m + tc.j) * g.bs;
-    const uint64_t off = (tc.chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
-    xor_members<NM, U, NT, T>(base, stride, par, lost, base + (uint64_t)lost * stride, off, g.bs,
-                              nm);
   }
 }
 
@@ -311,7 +306,9 @@ hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
 }
 
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
-                         const Geometry& g, const LaunchShape& ls, hipStream_t s) {
+                         const Geometry& g_class, const LaunchShape& ls, hipStream_t s) {
+  Geometry g = g_class;  // decode tiles are (stripe, chunk): see decode_kernel
+  g.total_tiles = g.S * g.tiles_per_block;
   const uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
   if (ls.threads == 256)
     return ls.nt ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s)

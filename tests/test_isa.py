@@ -51,7 +51,7 @@ def test_nt_kernels_use_nt_everywhere(kernels):
 
 
 @pytest.mark.parametrize("pattern", [r"encode_kernelILi16ELi1ELb1ELi64E",
-                                     r"decode_kernelILi16ELi2ELb1ELi64E",
+                                     r"decode_kernelILi16ELi1ELb1ELi64E",
                                      r"encode_kernelILi8ELi1ELb1ELi64E"])
 def test_benchmark_shapes_keep_full_occupancy(kernels, pattern):
     hits = [k for n, k in kernels.items() if re.search(pattern, n)]

@@ -26,7 +26,8 @@ from bench import WORKLOADS, algorithmic_bytes  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cfg3")
+    ap.add_argument("--workload", default="cfg3",
+                    help="bench.py workload name, or k,m,bs,S (e.g. 16,4,65536,4096)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--unroll", default="1,2")
@@ -43,7 +44,10 @@ def main():
 
     torch.cuda.set_device(0)
     assert xec.init(0) == 0
-    k, m, bs, S, _ = WORKLOADS[args.workload]
+    if args.workload in WORKLOADS:
+        k, m, bs, S, _ = WORKLOADS[args.workload]
+    else:
+        k, m, bs, S = (int(x) for x in args.workload.split(","))
     s = torch.cuda.current_stream()
     sets = []
     for i in range(2):
@@ -53,7 +57,7 @@ def main():
         assert xec.encode(d, p, S, bs, k, m, s) == 0
         sets.append((d, p))
     bm = np.ones((S, k + m), np.uint8)
-    bm[np.arange(S), (7 * np.arange(S)) % k] = 0
+    bm[np.arange(S), (7 * np.arange(S)) % k] = 0  # one lost data block per stripe
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     scratch = h_bm.to("cuda")
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
