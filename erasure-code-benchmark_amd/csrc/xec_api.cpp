@@ -12,8 +12,6 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
-#include <cstring>
-#include <vector>
 
 #include "xec_kernels.h"
 
@@ -47,12 +45,6 @@ xec::LaunchShape launch_shape(size_t bs) {
   return ls;
 }
 
-inline uint64_t load_u64(const uint8_t* p) {
-  uint64_t w;
-  std::memcpy(&w, p, 8);
-  return w;
-}
-
 }  // namespace
 
 extern "C" {
@@ -66,53 +58,7 @@ xec_status xec_check_args(const void* data, const void* parity, size_t bs, size_
   return XEC_SUCCESS;
 }
 
-// One pass over the whole S*(k+m)-byte bitmap, 8 bytes at a time.  Only bytes
-// with bit 0 clear are candidates for either rule:
-//   require_recovery: some DATA byte has bit 0 clear (popcount of byte & 1,
-//                     xorec_utils.hpp:144-149);
-//   is_recoverable:   per stripe, per class, at most one ZERO byte among the
-//                     class's data bytes and its parity byte (:160-175).
-// Candidates arrive in increasing position, so the stripe index advances
-// monotonically and the per-class marks are reset lazily per stripe.
-xec_status xec_check_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m, int* needs) {
-  if (needs) *needs = 0;
-  if (k < 1 || m < 1 || k % m != 0) return XEC_INVALID_COUNTS;
-  const size_t row = k + m;
-  const size_t n = S * row;
-  int need = 0;
-  size_t cur_stripe = 0, row_start = 0;
-  std::vector<uint32_t> mark(m, 0);  // stripe+1 that last marked each class
-  auto visit = [&](size_t pos) -> bool {
-    const uint8_t v = bm[pos];
-    if (v & 1u) return true;
-    while (pos >= row_start + row) {
-      row_start += row;
-      ++cur_stripe;
-    }
-    const size_t i = pos - row_start;
-    if (i < k) need = 1;
-    if (v != 0) return true;
-    const size_t cls = i < k ? (m == 1 ? 0 : i % m) : i - k;
-    const uint32_t tag = (uint32_t)cur_stripe + 1u;
-    if (mark[cls] == tag) return false;
-    mark[cls] = tag;
-    return true;
-  };
-  constexpr uint64_t kOnes = 0x0101010101010101ull;
-  size_t pos = 0;
-  for (; pos + 8 <= n; pos += 8) {
-    uint64_t even = ~load_u64(bm + pos) & kOnes;  // bit 0 clear -> low bit of byte set
-    while (even) {
-      int b = __builtin_ctzll(even) >> 3;
-      if (!visit(pos + (size_t)b)) return XEC_DECODE_FAILURE;
-      even &= even - 1;
-    }
-  }
-  for (; pos < n; ++pos)
-    if (!visit(pos)) return XEC_DECODE_FAILURE;
-  if (needs) *needs = need;
-  return XEC_SUCCESS;
-}
+// xec_check_bitmap lives in xec_scan.cpp (host-only, AVX2 where available).
 
 xec_status xec_init(int device_id) {
   int count = 0;

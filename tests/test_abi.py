@@ -106,6 +106,25 @@ def test_check_bitmap_random(oracle):
             assert got_need == want[1], (k, m, S, bm)
 
 
+@pytest.mark.parametrize("k,m", [(62, 2), (63, 1), (60, 4), (64, 1), (32, 32), (48, 16), (66, 2)])
+def test_check_bitmap_row_width_edges(oracle, k, m):
+    """Rows of 64 bytes take the per-stripe AVX2 path, wider rows the visitor;
+    both must agree with the oracle, including on the last stripes, whose
+    64-byte window would cross the end of the caller's buffer."""
+    rng = np.random.default_rng(k * 131 + m)
+    for trial in range(200):
+        S = int(rng.integers(1, 12))
+        p_loss = float(rng.choice([0.0, 0.01, 0.03, 0.2]))
+        bm = (rng.random((S, k + m)) >= p_loss).astype(np.uint8)
+        if trial % 3 == 0:
+            bm[rng.random((S, k + m)) < 0.05] = rng.choice([2, 3, 254, 255])
+        want = _oracle_batch_check(k, m, bm)
+        got_st, got_need = xec.check_bitmap(np.ascontiguousarray(bm.reshape(-1)), S, k, m)
+        assert int(got_st) == want[0], (k, m, S, bm)
+        if want[0] == xo.SUCCESS:
+            assert got_need == want[1], (k, m, S, bm)
+
+
 def test_check_bitmap_golden_patterns(known_answers):
     from conftest import GOLDEN
     for e in known_answers["decode"]:
