@@ -152,12 +152,18 @@ void enc_wave(const uint8_t* data, uint8_t* parity, Geo g) {
 // MODE 7: as 2, rebuilt block written to `out` at the same offset as in data (diagnostic)
 // MODE 8: as 2, rebuilt block written to stripe (c + S/2) % S's lost slot (diagnostic)
 // MODE 9: as 2, store with the default cache policy; MODE 10: store sc1 nt
+// MODE 7 with `out` = the other buffer set's data (lab.py d12): another data buffer
+// MODE 13: as 2, tiles in reverse order
+// MODE 14/15: as 2, rebuilt chunk written to chunk + tpb/2 / chunk + 4 of the
+// same lost block (diagnostic); MODE 16: to stripe c+1's lost slot; MODE 17:
+// into the parity block (diagnostic)
 template <int NM, int MODE>
 __global__ __launch_bounds__(64) void dec_wave(uint8_t* data, const uint8_t* parity,
                                                const uint8_t* lookup, uint8_t* out, Geo g) {
   const uint32_t lane = threadIdx.x;
   const uint64_t stride = g.m * g.bs;
-  for (uint64_t t = blockIdx.x; t < g.total; t += gridDim.x) {
+  for (uint64_t t0 = blockIdx.x; t0 < g.total; t0 += gridDim.x) {
+    const uint64_t t = MODE == 13 ? g.total - 1 - t0 : t0;
     uint64_t c, j, chunk;
     decompose<64>(t, MODE == 6 ? 1 : 0, g, c, j, chunk);
     int lost;
@@ -196,6 +202,13 @@ __global__ __launch_bounds__(64) void dec_wave(uint8_t* data, const uint8_t* par
     uint8_t* dst = data + (c * g.k + j) * g.bs + lost * stride;
     if (MODE == 3) dst = out + c * g.bs;
     if (MODE == 7) dst = out + (c * g.k + j) * g.bs + lost * stride;
+    if (MODE == 14) dst = data + (c * g.k + j) * g.bs + lost * stride + ((chunk + g.tpb / 2) % g.tpb) * 1024 - chunk * 1024;
+    if (MODE == 15) dst = data + (c * g.k + j) * g.bs + lost * stride + ((chunk + 4) % g.tpb) * 1024 - chunk * 1024;
+    if (MODE == 16) {
+      const uint64_t c2 = (c + 1) % g.S;
+      dst = data + (c2 * g.k + j) * g.bs + ((7 * c2) % g.k) * stride;
+    }
+    if (MODE == 17) dst = const_cast<uint8_t*>(parity) + (c * g.m + j) * g.bs;
     if (MODE == 8) {
       const uint64_t c2 = (c + g.S / 2) % g.S;
       dst = data + (c2 * g.k + j) * g.bs + ((7 * c2) % g.k) * stride;
@@ -264,6 +277,69 @@ __global__ __launch_bounds__(64) void enc_seq(const uint8_t* data, uint8_t* pari
   }
 }
 
+// LDS staging (the north star's suggested shape): four waves each reduce four
+// of the 16 members of a 1 KiB column, stage the partial in LDS, and wave 0
+// combines the four partials and stores.
+__global__ __launch_bounds__(256) void enc_lds(const uint8_t* data, uint8_t* parity, Geo g) {
+  __shared__ u32x4 part[4][64];
+  const uint64_t t = blockIdx.x;
+  if (t >= g.total) return;
+  uint64_t c, j, chunk;
+  decompose<64>(t, 0, g, c, j, chunk);
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t off = (chunk * 64 + lane) * 16;
+  const uint8_t* base = data + (c * g.k + j) * g.bs + off;
+  const uint64_t stride = g.m * g.bs;
+  u32x4 v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + (w * 4 + r) * stride));
+  part[w][lane] = v[0] ^ v[1] ^ v[2] ^ v[3];
+  __syncthreads();
+  if (w == 0) {
+    const u32x4 acc = part[0][lane] ^ part[1][lane] ^ part[2][lane] ^ part[3][lane];
+    uint8_t* dst = parity + (c * g.m + j) * g.bs;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (uint32_t)off, 0, 2);
+  }
+}
+
+// Wavefront shuffle reduction (member-split across lanes): each load
+// instruction covers 8 members x 128 B (8 lanes per member), two cover the
+// 16 members of a 128 B column; after XOR-ing the two, the 8 member groups are
+// folded with lane-xor shuffles 8/16/32 and lanes 0-7 store 128 B.  Eight
+// such columns make the 1 KiB tile; all 16 loads per lane are in flight.
+__global__ __launch_bounds__(64) void enc_shfl(const uint8_t* data, uint8_t* parity, Geo g) {
+  const uint64_t t = blockIdx.x;
+  if (t >= g.total) return;
+  uint64_t c, j, chunk;
+  decompose<64>(t, 0, g, c, j, chunk);
+  const uint32_t lane = threadIdx.x, sub = lane & 7, grp = lane >> 3;
+  const uint64_t stride = g.m * g.bs;
+  const uint8_t* base = data + (c * g.k + j) * g.bs + chunk * 1024 + sub * 16;
+  u32x4 a[8], b[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    a[s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + grp * stride + s * 128));
+    b[s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + (grp + 8) * stride + s * 128));
+  }
+  uint8_t* dst = parity + (c * g.m + j) * g.bs;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    u32x4 x = a[s] ^ b[s];
+#pragma unroll
+    for (int mask = 8; mask < 64; mask <<= 1) {
+      x.x ^= (uint32_t)__shfl_xor((int)x.x, mask, 64);
+      x.y ^= (uint32_t)__shfl_xor((int)x.y, mask, 64);
+      x.z ^= (uint32_t)__shfl_xor((int)x.z, mask, 64);
+      x.w ^= (uint32_t)__shfl_xor((int)x.w, mask, 64);
+    }
+    if (grp == 0)
+      __builtin_amdgcn_raw_buffer_store_b128(x, rs, (uint32_t)(chunk * 1024 + s * 128 + sub * 16), 0, 2);
+  }
+}
+
 namespace {
 template <int THREADS>
 Geo geo(uint64_t S, uint64_t bs, uint64_t k, uint64_t m) {
@@ -323,7 +399,8 @@ const char* lab_variant_name(int v) {
       "M_buf_sc1_nt_256",  "N_persist_db_4096", "O_buf_nt_sc1nt_256", "P_wave_u1_w8",
       "Q_wave_u1_w7",      "R_wave_u1_w6",      "S_wave_u1_w4",       "T_wave_u2_w4",
       "U_wave_u2_w5",      "V_wave_u2_w3",      "W_wave_u1_w5",       "X_seq_tpw1",
-      "Y_seq_tpw2",        "Z_seq_tpw4"};
+      "Y_seq_tpw2",        "Z_seq_tpw4",        "AA_lds_stage_256",   "AB_shfl_8x128_64",
+      "AC_xcd_contig_64",  "AD_chunk_fast_64"};
   return (v >= 0 && v < (int)(sizeof names / sizeof *names)) ? names[v] : nullptr;
 }
 
@@ -331,8 +408,10 @@ const char* lab_dec_name(int v) {
   static const char* names[] = {"d0_ballot", "d1_table", "d2_computed", "d3_computed_sepout",
                                 "d4_table_gs8192", "d5_ballot_gs8192", "d6_stripe_first",
                                 "d7_out_same_offset", "d8_far_stripe", "d9_store_default",
-                                "d10_store_sc1nt", "d11_scalar_lookup"};
-  return (v >= 0 && v < 12) ? names[v] : nullptr;
+                                "d10_store_sc1nt", "d11_scalar_lookup", "d12_other_set_data",
+                                "d13_reverse_order", "d14_chunk_half_shift", "d15_chunk_4k_shift",
+                                "d16_next_stripe", "d17_into_parity"};
+  return (v >= 0 && v < 18) ? names[v] : nullptr;
 }
 
 // Bandwidth ceilings on the encode's geometry (k = 16, m = 1): 0 read-only
@@ -365,6 +444,12 @@ int lab_decode(int v, void* d, const void* p, const void* lookup, void* out, uin
     case 9: return launch_dec<9>(d, p, lookup, out, S, bs, k, m, 0, s);
     case 10: return launch_dec<10>(d, p, lookup, out, S, bs, k, m, 0, s);
     case 11: return launch_dec<11>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 12: return launch_dec<7>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 13: return launch_dec<13>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 14: return launch_dec<14>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 15: return launch_dec<15>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 16: return launch_dec<16>(d, p, lookup, out, S, bs, k, m, 0, s);
+    case 17: return launch_dec<17>(d, p, lookup, out, S, bs, k, m, 0, s);
   }
   return 1;
 }
@@ -400,6 +485,20 @@ int lab_encode(int v, const void* d, void* p, uint64_t S, uint64_t bs, uint64_t 
     case 23: return launch_seq<16, 1>(d, p, S, bs, k, m, s);
     case 24: return launch_seq<16, 2>(d, p, S, bs, k, m, s);
     case 25: return launch_seq<16, 4>(d, p, S, bs, k, m, s);
+    case 26: {
+      if (bs % 1024) return 1;
+      Geo g = geo<64>(S, bs, k, m);
+      enc_lds<<<(uint32_t)g.total, 256, 0, s>>>(static_cast<const uint8_t*>(d), static_cast<uint8_t*>(p), g);
+      return hipGetLastError() == hipSuccess ? 0 : 6;
+    }
+    case 27: {
+      if (bs % 1024) return 1;
+      Geo g = geo<64>(S, bs, k, m);
+      enc_shfl<<<(uint32_t)g.total, 64, 0, s>>>(static_cast<const uint8_t*>(d), static_cast<uint8_t*>(p), g);
+      return hipGetLastError() == hipSuccess ? 0 : 6;
+    }
+    case 28: return launch<16, 64, 2, GLOBAL_NT, 2>(d, p, S, bs, k, m, s);
+    case 29: return launch<16, 64, 0, GLOBAL_NT, 2>(d, p, S, bs, k, m, s);
   }
   return 1;
 }
