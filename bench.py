@@ -23,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -274,8 +275,10 @@ def main():
         dist.barrier()
     assert rc == 0, "xec call failed inside the timed region"
     elapsed = t1 - t0
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    enc_list = [e[0].elapsed_time(e[1]) for e in events]
+    dec_list = [e[1].elapsed_time(e[2]) for e in events]
+    enc_ms = sum(enc_list) / args.steps
+    dec_ms = sum(dec_list) / args.steps
 
     # ---- correctness of what was timed -------------------------------------
     # parity == XOR of each class's data (encode), then erase -> decode ->
@@ -344,6 +347,12 @@ def main():
             "data_GBps_reference_convention": round(
                 2 * args.steps * S_per * k * bs * world / elapsed / 1e9, 2),
             "verified": bad == 0.0,
+            # per-launch HIP-event statistics on rank 0 (median with stddev)
+            "launch_stats_rank0": {
+                n: {"mean_ms": round(statistics.fmean(v), 4), "median_ms": round(statistics.median(v), 4),
+                    "stdev_ms": round(statistics.stdev(v), 4) if len(v) > 1 else 0.0,
+                    "min_ms": round(min(v), 4), "max_ms": round(max(v), 4)}
+                for n, v in (("encode", enc_list), ("decode", dec_list))},
         }
         if traffic_src:
             out["roofline"]["traffic_source"] = traffic_src.get("source")

@@ -101,6 +101,26 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
              : XEC_DEVICE_ERROR;
 }
 
+xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
+                             size_t m, const uint8_t* d_bitmap, int32_t* d_status,
+                             hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
+  if (st != XEC_SUCCESS) return st;
+  if (d_status == nullptr || reinterpret_cast<uintptr_t>(d_status) % 4 != 0)
+    return XEC_INVALID_ALIGNMENT;
+  if (hipMemsetAsync(d_status, 0, sizeof(int32_t), stream) != hipSuccess) return XEC_DEVICE_ERROR;
+  if (S == 0) return XEC_SUCCESS;
+  if (d_bitmap == nullptr) return XEC_INVALID_ALIGNMENT;
+  const xec::LaunchShape ls = launch_shape(bs);
+  xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+  if (xec::launch_check(d_bitmap, g, d_status, stream) != hipSuccess) return XEC_DEVICE_ERROR;
+  g.gate = d_status;
+  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
+             ? XEC_SUCCESS
+             : XEC_DEVICE_ERROR;
+}
+
 xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k, size_t m,
                      const uint8_t* d_bitmap, hipStream_t stream) {
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;

@@ -15,6 +15,7 @@ struct Geometry {
   uint64_t bs;               // bytes per block
   uint64_t tiles_per_block;  // ceil(bs / (16 * threads * unroll))
   uint64_t total_tiles;      // S * m * tiles_per_block
+  const int32_t* gate;       // decode only: skip all work if *gate != 0 (nullptr = no gate)
 };
 
 struct LaunchShape {
@@ -35,6 +36,7 @@ inline Geometry make_geometry(uint64_t S, uint64_t bs, uint64_t k, uint64_t m,
   const uint64_t tile_bytes = 16ull * (uint64_t)ls.threads * (uint64_t)ls.unroll;
   g.tiles_per_block = (bs + tile_bytes - 1) / tile_bytes;
   g.total_tiles = S * m * g.tiles_per_block;
+  g.gate = nullptr;
   return g;
 }
 
@@ -48,6 +50,11 @@ hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
                          const LaunchShape& ls, hipStream_t s);
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
                          const Geometry& g, const LaunchShape& ls, hipStream_t s);
+// Device-side recoverability check (xorec_utils.hpp:160-175 over the batch):
+// *d_status |= 4 if some class of some stripe lost two or more blocks.  The
+// caller zeroes *d_status first (stream-ordered).
+hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
+                        hipStream_t s);
 hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, const Geometry& g,
                         hipStream_t s);
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,

@@ -35,6 +35,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // pointer into the constant address space: uniform loads through it become
 // scalar (s_load) loads served by the scalar cache
 typedef const uint32_t __attribute__((address_space(4)))* const_u32_as4;
+typedef const int32_t __attribute__((address_space(4)))* const_i32_as4;
 
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -169,6 +170,9 @@ __global__ __launch_bounds__(T) void encode_kernel(const uint8_t* __restrict__ d
 template <int NM, int U, bool NT, int T>
 __global__ __launch_bounds__(T) void decode_kernel(uint8_t* data, const uint8_t* __restrict__ parity,
                                                    const uint8_t* __restrict__ bitmap, Geometry g) {
+  // xec_decode_device: the check kernel ran first on this stream; a failed
+  // batch is left untouched (all-or-nothing, xorec_gpu_cmp.cu:75-81).
+  if (g.gate != nullptr && *(const_i32_as4)g.gate != 0) return;
   const uint32_t nm = NM > 0 ? (uint32_t)NM : (uint32_t)g.nm;
   const uint32_t m = (uint32_t)g.m;
   const uint64_t stride = g.m * g.bs;
@@ -194,6 +198,24 @@ __global__ __launch_bounds__(T) void decode_kernel(uint8_t* data, const uint8_t*
                                   base + (uint64_t)r * stride, off, g.bs, nm);
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// check: one thread per (stripe, class); counts the class's lost blocks among
+// its k/m data bytes and its parity byte (is_recoverable, xorec_utils.hpp:160-175).
+// Failure is rare, so the atomic is off the common path.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void check_kernel(const uint8_t* __restrict__ bitmap, Geometry g,
+                                                    int32_t* status) {
+  const uint64_t items = g.S * g.m, row = g.k + g.m;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < items;
+       t += (uint64_t)gridDim.x * 256) {
+    const uint64_t c = t / g.m, j = t % g.m;
+    const uint8_t* r = bitmap + c * row;
+    uint32_t lost = r[g.k + j] == 0;
+    for (uint64_t i = j; i < g.k; i += g.m) lost += r[i] == 0;
+    if (lost > 1) atomicOr(status, 4 /* XEC_DECODE_FAILURE */);
   }
 }
 
@@ -315,6 +337,13 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
                  : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s);
   return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s)
                : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s);
+}
+
+hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
+                        hipStream_t s) {
+  const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192);
+  check_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status);
+  return hipGetLastError();
 }
 
 hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, const Geometry& g,

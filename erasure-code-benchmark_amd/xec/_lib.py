@@ -25,6 +25,7 @@ EXPORTED = (
     "xec_erase", "xec_fill_splitmix64", "xec_set_launch", "xec_status_string",
     "xec_build_info", "xec_pipeline_create", "xec_pipeline_destroy", "xec_pipeline_encode",
     "xec_pipeline_decode", "xec_write_validation_pattern", "xec_validate_blocks",
+    "xec_decode_device",
 )
 
 
@@ -85,6 +86,7 @@ def lib() -> ctypes.CDLL:
         "xec_pipeline_decode": ([vp, vp, vp, sz, vp], st),
         "xec_write_validation_pattern": ([vp, sz, sz, ctypes.c_uint64, vp], st),
         "xec_validate_blocks": ([vp, sz, sz, vp, vp], st),
+        "xec_decode_device": ([vp, vp, sz, sz, sz, sz, vp, vp, vp], st),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

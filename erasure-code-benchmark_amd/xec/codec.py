@@ -48,6 +48,14 @@ def decode(d_data, d_parity, S: int, bs: int, k: int, m: int, h_bitmap, d_bitmap
                                    _ptr(d_bitmap), _stream(stream)))
 
 
+def decode_device(d_data, d_parity, S: int, bs: int, k: int, m: int, d_bitmap, d_status,
+                  stream=None) -> Status:
+    """xec_decode_device -- bitmap already on the device; batch verdict lands in
+    d_status (int32 device tensor: 0 or 4) in stream order, nothing is synchronised."""
+    return Status(lib().xec_decode_device(_ptr(d_data), _ptr(d_parity), S, bs, k, m,
+                                          _ptr(d_bitmap), _ptr(d_status), _stream(stream)))
+
+
 def erase(d_data, d_parity, S: int, bs: int, k: int, m: int, d_bitmap, stream=None) -> Status:
     """xec_erase -- device-side simulate_data_loss (abstract_bm.cpp:20-39)."""
     return Status(lib().xec_erase(_ptr(d_data), _ptr(d_parity), S, bs, k, m, _ptr(d_bitmap),

@@ -79,6 +79,22 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                       size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream);
 
+/* Device-resident form of xec_decode (no reference counterpart: the reference
+ * always scans a host bitmap, xorec_gpu_cmp.cu:75-83).  For callers whose
+ * erasure bitmap already lives in device memory: no host scan, no copy, no
+ * host synchronisation, so the call can be captured in a hipGraph.
+ * Enqueues on `stream`: *d_status = 0; a check kernel that sets *d_status = 4
+ * (XEC_DECODE_FAILURE) if any stripe is unrecoverable (is_recoverable,
+ * xorec_utils.hpp:160-175); then the decode kernel, which does nothing if
+ * *d_status != 0 (all-or-nothing, like xec_decode) and otherwise rebuilds
+ * every lost data block exactly as xec_decode does.  The return value covers
+ * only what the host can check (argument errors as xec_decode, d_status
+ * null or not 4-B aligned -> XEC_INVALID_ALIGNMENT, launch failure); the batch
+ * verdict is *d_status (device int32), valid once the stream reaches it. */
+xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
+                             size_t m, const uint8_t* d_bitmap, int32_t* d_status,
+                             hipStream_t stream);
+
 /* Host-only recoverability scan used by xec_decode (no GPU needed):
  * returns XEC_DECODE_FAILURE if some stripe is unrecoverable, else
  * XEC_SUCCESS and sets *needs_recovery to 1 iff some stripe needs recovery. */

@@ -1,0 +1,166 @@
+"""xec_decode_device: the device-resident decode (bitmap already in HBM, verdict
+in a device int32, no host scan or copy) against the oracle and against the
+host-bitmap xec_decode on the same inputs, plus hipGraph capture.
+
+The batch verdict follows the reference's all-or-nothing rule
+(xorec_gpu_cmp.cu:75-81, is_recoverable xorec_utils.hpp:160-175): 4 and
+nothing written if any stripe lost two blocks of one class.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import xorec_oracle as xo
+from conftest import GOLDEN
+from test_gpu_parity import Batch, encode_and_check
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _device_decode(xec, b, bm: np.ndarray, status_init: int = 0x7F):
+    """erase per bm, then xec_decode_device; returns (verdict, data, parity, erased data)."""
+    torch = _torch()
+    d_bm = torch.from_numpy(np.ascontiguousarray(bm)).to("cuda")
+    d_status = torch.full((1,), status_init, dtype=torch.int32, device="cuda")
+    assert xec.erase(b.d, b.p, b.S, b.bs, b.k, b.m, d_bm, b.stream) == 0
+    erased = b.data()
+    erased_p = b.parity()
+    assert xec.decode_device(b.d, b.p, b.S, b.bs, b.k, b.m, d_bm, d_status, b.stream) == 0
+    torch.cuda.synchronize()
+    got_p = b.parity()
+    assert np.array_equal(got_p, erased_p), "decode_device wrote parity"
+    return int(d_status.item()), b.data(), erased
+
+
+def test_golden_decode_fixtures_device(gpu, oracle, known_answers):
+    for e in known_answers["decode"]:
+        k, m, bs, S = e["k"], e["m"], e["bs"], e["S"]
+        bm = np.fromfile(GOLDEN / "patterns" / e["pattern"], dtype=np.uint8)
+        b, ref_d, _ = encode_and_check(gpu, oracle, S, k, m, bs, known_answers["seed"])
+        verdict, got, erased = _device_decode(gpu, b, bm)
+        if "4" in e["codes"]:
+            assert verdict == gpu.Status.DECODE_FAILURE, e
+            assert np.array_equal(got, erased), "failed batch was modified"
+        else:
+            assert verdict == gpu.Status.SUCCESS, e
+            assert np.array_equal(got, ref_d), e
+            assert f"{oracle.fnv1a64(got):016x}" == e["data_fnv_after"]
+
+
+@pytest.mark.parametrize("k,m", [(4, 1), (16, 1), (8, 4), (12, 3), (40, 8), (6, 6), (66, 2)])
+def test_random_patterns_match_oracle_and_host_decode(gpu, oracle, k, m):
+    """Same verdict and bytes as the oracle's all-or-nothing batch decode and as
+    xec_decode (host scan), on random loss patterns including unrecoverable
+    ones and bitmap bytes that are neither 0 nor 1."""
+    torch = _torch()
+    rng = np.random.default_rng(k * 7 + m)
+    bs = 1024
+    for trial in range(12):
+        S = int(rng.integers(1, 24))
+        seed = 500 + trial
+        p_loss = float(rng.choice([0.0, 0.03, 0.1, 0.25]))
+        bm = (rng.random((S, k + m)) >= p_loss).astype(np.uint8)
+        if trial % 3 == 0:
+            bm[rng.random((S, k + m)) < 0.05] = rng.choice([2, 3, 255])
+        rows = bm
+        bm = np.ascontiguousarray(bm.reshape(-1))
+        # oracle: erase (zero lost blocks) then all-or-nothing batch decode
+        ref_d, ref_p = oracle.batch(S, k, m, bs, seed_base=seed)
+        o_d, o_p = ref_d.reshape(S, k, bs).copy(), ref_p.reshape(S, m, bs).copy()
+        o_d[rows[:, :k] == 0] = 0
+        o_p[rows[:, k:] == 0] = 0
+        od, op = oracle.aligned(o_d.size), oracle.aligned(o_p.size)
+        od[:], op[:] = o_d.reshape(-1), o_p.reshape(-1)
+        want = oracle.decode_batch_all_or_nothing(od, op, S, bs, k, m, bm)
+
+        host = Batch(gpu, S, k, m, bs, seed=seed)
+        dev = Batch(gpu, S, k, m, bs, seed=seed)
+        assert gpu.encode(host.d, host.p, S, bs, k, m, host.stream) == 0
+        assert gpu.encode(dev.d, dev.p, S, bs, k, m, dev.stream) == 0
+        h_bm = torch.from_numpy(bm).pin_memory()
+        d_bm = h_bm.to("cuda")
+        assert gpu.erase(host.d, host.p, S, bs, k, m, d_bm, host.stream) == 0
+        st_host = gpu.decode(host.d, host.p, S, bs, k, m, h_bm, torch.empty_like(d_bm),
+                             host.stream)
+        verdict, got, _ = _device_decode(gpu, dev, bm)
+        assert verdict == want == int(st_host), (k, m, S, rows)
+        assert np.array_equal(got, od), (k, m, S, rows)
+        assert np.array_equal(host.data(), od)
+        assert np.array_equal(dev.parity(), op)
+
+
+def test_full_size_cfg3_device(gpu):
+    """BASELINE configs[2] at full size (4 GiB): rebuilt data == a fresh fill."""
+    torch = _torch()
+    S, k, m, bs = 256, 16, 1, 1 << 20
+    b = Batch(gpu, S, k, m, bs)
+    assert gpu.encode(b.d, b.p, S, bs, k, m, b.stream) == 0
+    bm = xo.single_erasure_bitmap(S, k, m)
+    d_bm = torch.from_numpy(bm).to("cuda")
+    d_status = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == 0
+    assert gpu.decode_device(b.d, b.p, S, bs, k, m, d_bm, d_status, b.stream) == 0
+    fresh = torch.empty_like(b.d)
+    assert gpu.fill_splitmix64(fresh, S, k * bs, xo.RANDOM_SEED, b.stream) == 0
+    torch.cuda.synchronize()
+    assert int(d_status.item()) == 0
+    assert torch.equal(fresh, b.d)
+
+
+def test_graph_capture_encode_erase_decode(gpu, oracle):
+    """The device-resident path has no host work, so one hipGraph can hold
+    encode -> erase -> decode; replays are bit-exact against the oracle."""
+    torch = _torch()
+    S, k, m, bs = 12, 8, 2, 4096
+    ref_d, ref_p = oracle.batch(S, k, m, bs, seed_base=xo.RANDOM_SEED)
+    b = Batch(gpu, S, k, m, bs)
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(S):
+        oracle.select_lost_blocks(k, m, m, bm[c], 77 + c)
+    d_bm = torch.from_numpy(bm.reshape(-1)).to("cuda")
+    d_status = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        s = torch.cuda.current_stream()
+        assert gpu.encode(b.d, b.p, S, bs, k, m, s) == 0
+        assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, s) == 0
+        assert gpu.decode_device(b.d, b.p, S, bs, k, m, d_bm, d_status, s) == 0
+    for _ in range(2):
+        d_status.fill_(-1)
+        b.d[: S * k * bs].copy_(torch.from_numpy(ref_d).to("cuda"))
+        b.p.fill_(0xEE)
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(d_status.item()) == 0
+        assert np.array_equal(b.data(), ref_d)
+        want_p = ref_p.reshape(S, m, bs).copy()
+        want_p[bm[:, k:] == 0] = 0  # erase zeroed the lost parity; decode never rebuilds it
+        assert np.array_equal(b.parity().reshape(S, m, bs), want_p)
+
+
+def test_device_argument_errors_and_empty_batch(gpu):
+    torch = _torch()
+    S_ = gpu.Status
+    d = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    p = torch.zeros(1 << 14, dtype=torch.uint8, device="cuda")
+    bm = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    st = torch.full((4,), 9, dtype=torch.int32, device="cuda")
+    assert gpu.decode_device(d, p, 1, 4096, 4, 1, bm, st.data_ptr() + 2) == S_.INVALID_ALIGNMENT
+    assert gpu.decode_device(d, p, 1, 4096, 4, 1, bm, 0) == S_.INVALID_ALIGNMENT
+    assert gpu.decode_device(d, p, 1, 100, 4, 1, bm, st) == S_.INVALID_SIZE
+    assert gpu.decode_device(d.data_ptr() + 16, p, 1, 4096, 4, 1, bm, st) == S_.INVALID_ALIGNMENT
+    assert gpu.decode_device(d, p, 1, 4096, 6, 4, bm, st) == S_.INVALID_COUNTS
+    torch.cuda.synchronize()
+    assert st.tolist() == [9, 9, 9, 9], "argument errors must enqueue nothing"
+    assert gpu.decode_device(d, p, 0, 4096, 4, 1, bm, st) == S_.SUCCESS
+    torch.cuda.synchronize()
+    assert st.tolist() == [0, 9, 9, 9]
+    assert int(d.sum()) == 0 and int(p.sum()) == 0
