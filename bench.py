@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-scatter", action="store_true",
                     help="skip the N>1 scatter-inclusive measurement (RCCL send/recv)")
     ap.add_argument("--scatter-timeout", type=float, default=120.0)
+    ap.add_argument("--decode-api", default="host", choices=["host", "device"],
+                    help="host: xec_decode (reference-shaped: host bitmap scan + H2D copy); "
+                         "device: xec_decode_device (bitmap resident, verdict on the device)")
     return ap.parse_args()
 
 
@@ -239,6 +242,7 @@ def main():
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     d_bm = h_bm.to("cuda")
     scratch = [torch.empty_like(d_bm) for _ in range(2)]
+    d_status = torch.full((2,), -1, dtype=torch.int32, device="cuda")
     # The lost block's content on entry to decode is irrelevant (include/xec.h),
     # so the timed loop does not re-erase: every decode still reads k/m-1
     # survivors + parity and rewrites the lost block.  Erasure + rebuild is
@@ -253,7 +257,10 @@ def main():
         rc = xec.encode(de, pe, S, bs, k, m, stream)
         if ev is not None:
             ev[1].record(stream)
-        rc |= xec.decode(dd, pd, S, bs, k, m, h_bm, scratch[(i + 1) % 2], stream)
+        if args.decode_api == "device":
+            rc |= xec.decode_device(dd, pd, S, bs, k, m, d_bm, d_status[(i + 1) % 2:], stream)
+        else:
+            rc |= xec.decode(dd, pd, S, bs, k, m, h_bm, scratch[(i + 1) % 2], stream)
         if ev is not None:
             ev[2].record(stream)
         return rc
@@ -274,6 +281,8 @@ def main():
     if world > 1:
         dist.barrier()
     assert rc == 0, "xec call failed inside the timed region"
+    if args.decode_api == "device":
+        assert d_status.tolist() == [0, 0], f"device decode verdicts {d_status.tolist()}"
     elapsed = t1 - t0
     enc_list = [e[0].elapsed_time(e[1]) for e in events]
     dec_list = [e[1].elapsed_time(e[2]) for e in events]
@@ -333,7 +342,9 @@ def main():
                        "stripes_per_gpu": S_per, "stripes_total": S_total,
                        "erasure": "data block (7c) mod k lost per stripe",
                        "parallelism": f"stripe-partition x{world} (no data-path collective)",
-                       "bytes_convention": "algorithmic: enc S(k+m)bs + dec S(k/m+1)bs"},
+                       "bytes_convention": "algorithmic: enc S(k+m)bs + dec S(k/m+1)bs",
+                       "decode_api": "xec_decode_device" if args.decode_api == "device"
+                       else "xec_decode"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "kernel": "xec::encode_kernel",

@@ -42,3 +42,13 @@ def test_bench_json_line(workload, stripes):
     c = out["cpu_baseline"]
     assert c["kind"] in ("reference", "port") and c["cores"] >= 1 and c["value"] > 0
     assert out["value"] > 0
+
+
+def test_bench_device_decode_api():
+    out = run_bench("--workload", "cfg2", "--stripes", "64", "--steps", "3", "--warmup", "1",
+                    "--no-cpu-baseline", "--decode-api", "device")
+    assert out["verified"] is True and out["value"] > 0
+    assert out["config"]["decode_api"] == "xec_decode_device"
+    stats = out["launch_stats_rank0"]
+    assert set(stats) == {"encode", "decode"}
+    assert stats["decode"]["min_ms"] <= stats["decode"]["median_ms"] <= stats["decode"]["max_ms"]
