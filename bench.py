@@ -123,16 +123,9 @@ def cpu_baseline_reference(k, m, bs, budget_s, threads, S):
             "cpu_model": model}
 
 
-def cpu_baseline(k, m, bs, budget_s):
-    """The reference CPU path (xorec_bm.cpp:27-58, OpenMP over stripes) timed on
-    this host on a bounded sample of the same workload: the reference's own code
-    when oracle/_ref was built, else the oracle's C restatement ("port")."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
-    S = max(1, (1 << 30) // (k * bs))  # ~1 GiB of data: beyond any host LLC
-    ref = cpu_baseline_reference(k, m, bs, budget_s, threads, S)
-    if ref is not None:
-        return ref
+def cpu_baseline_port(k, m, bs, budget_s, threads, S):
+    """Fallback when oracle/_ref is absent: the oracle's C restatement of the
+    same loop ("port")."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import xorec_oracle as xo  # the CPU baseline leg is the only bench use of oracle/
 
@@ -147,12 +140,31 @@ def cpu_baseline(k, m, bs, budget_s):
         assert o.decode_batch(data, parity, S, bs, k, m, bm, threads) == 0
         t_tot += time.perf_counter() - t0
         reps += 1
-    cpu_model = _cpu_model()[0]
     return {"value": round(reps * (b_enc + b_dec) / t_tot / 1e9, 2), "unit": "GB/s",
             "cores": threads, "kind": "port",
             "sample": f"{reps} x (encode+decode) of {S} stripes k={k}+{m} {bs >> 10} KiB "
                       f"(oracle/xorec_oracle.c, OpenMP over stripes), {t_tot:.1f} s wall",
-            "cpu_model": cpu_model}
+            "cpu_model": _cpu_model()[0]}
+
+
+def cpu_baseline(k, m, bs, budget_s):
+    """The reference CPU path (xorec_bm.cpp:27-58, OpenMP over stripes) timed on
+    this host on a bounded sample of the same workload: the reference's own code
+    when oracle/_ref was built, else the oracle's C restatement ("port").  Also
+    a short single-thread run of the same code."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    S = max(1, (1 << 30) // (k * bs))  # ~1 GiB of data: beyond any host LLC
+    S1 = max(1, (256 << 20) // (k * bs))
+    out = cpu_baseline_reference(k, m, bs, budget_s, threads, S)
+    if out is not None:
+        one = cpu_baseline_reference(k, m, bs, min(2.0, budget_s), 1, S1)
+    else:
+        out = cpu_baseline_port(k, m, bs, budget_s, threads, S)
+        one = cpu_baseline_port(k, m, bs, min(2.0, budget_s), 1, S1)
+    if one is not None:
+        out["single_thread"] = {"value": one["value"], "unit": one["unit"], "sample": one["sample"]}
+    return out
 
 
 def measure_scatter(torch, dist, xec, S_total, S, start, k, m, bs, stream, enc_ms, reps=3):
@@ -360,7 +372,8 @@ def main():
             "verified": bad == 0.0,
             # per-launch HIP-event statistics on rank 0 (median with stddev)
             "launch_stats_rank0": {
-                n: {"mean_ms": round(statistics.fmean(v), 4), "median_ms": round(statistics.median(v), 4),
+                n: {"mean_ms": round(statistics.fmean(v), 4),
+                    "median_ms": round(statistics.median(v), 4),
                     "stdev_ms": round(statistics.stdev(v), 4) if len(v) > 1 else 0.0,
                     "min_ms": round(min(v), 4), "max_ms": round(max(v), 4)}
                 for n, v in (("encode", enc_list), ("decode", dec_list))},
