@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""In-process A/B of two or more builds of libxec_hip.so (tools/ab/build_rev.sh)
+on one MI355X: same buffers, interleaved rounds, HIP events on the launching
+stream -- so box-to-box spread (±3-4 %) cannot masquerade as a kernel change.
+
+    python tools/ab/ab.py --libs base,new --workload cfg4 [--rounds 7 --iters 10]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
+
+from bench import WORKLOADS, algorithmic_bytes  # noqa: E402
+
+
+def load(name: str):
+    L = ctypes.CDLL(str(ROOT / "tools" / "ab" / f"libxec_{name}.so"))
+    sz, vp = ctypes.c_size_t, ctypes.c_void_p
+    L.xec_init.argtypes = [ctypes.c_int]
+    L.xec_encode.argtypes = [vp, vp, sz, sz, sz, sz, vp]
+    L.xec_decode.argtypes = [vp, vp, sz, sz, sz, sz, vp, vp, vp]
+    assert L.xec_init(0) == 0
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--workload", default="cfg3",
+                    help="bench.py workload name, or k,m,bs,S")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import xec  # for the shared fill; torch first, so all libs share its HIP runtime
+
+    torch.cuda.set_device(0)
+    assert xec.init(0) == 0
+    libs = {n: load(n) for n in args.libs.split(",")}
+    if args.workload in WORKLOADS:
+        k, m, bs, S, _ = WORKLOADS[args.workload]
+    else:
+        k, m, bs, S = (int(x) for x in args.workload.split(","))
+    s = torch.cuda.current_stream()
+    sh = ctypes.c_void_p(s.cuda_stream)
+    sets = []
+    for i in range(2):
+        d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+        p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+        assert xec.fill_splitmix64(d, S, k * bs, 1896 + 7919 * i, s) == 0
+        sets.append((d, p))
+    bm = np.ones((S, k + m), np.uint8)
+    bm[np.arange(S), (7 * np.arange(S)) % k] = 0
+    h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
+    scratch = h_bm.to("cuda")
+    b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
+
+    # every build must produce the same parity and the same rebuilt data
+    ref = None
+    for n, L in libs.items():
+        d, p = sets[0]
+        assert L.xec_encode(d.data_ptr(), p.data_ptr(), S, bs, k, m, sh) == 0
+        assert L.xec_decode(d.data_ptr(), p.data_ptr(), S, bs, k, m, h_bm.data_ptr(),
+                            scratch.data_ptr(), sh) == 0
+        torch.cuda.synchronize()
+        got = (p.clone(), d.clone())
+        if ref is None:
+            ref = got
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), n
+    del ref, got
+
+    def run(fn):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
+        fn(0)
+        ev[0].record(s)
+        for i in range(args.iters):
+            fn(i + 1)
+            ev[i + 1].record(s)
+        torch.cuda.synchronize()
+        return [ev[i].elapsed_time(ev[i + 1]) for i in range(args.iters)]
+
+    res = {n: {"enc": [], "dec": []} for n in libs}
+    for _ in range(args.rounds):
+        for n, L in libs.items():
+            res[n]["enc"] += run(lambda i, L=L: L.xec_encode(
+                sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
+            res[n]["dec"] += run(lambda i, L=L: L.xec_decode(
+                sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(), S, bs, k, m,
+                h_bm.data_ptr(), scratch.data_ptr(), sh))
+    out = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S, "libs": {}}
+    for n, r in res.items():
+        e, d = statistics.median(r["enc"]), statistics.median(r["dec"])
+        out["libs"][n] = {"enc_ms_med": round(e, 4), "enc_GBps": round(b_enc / e / 1e6, 1),
+                          "dec_ms_med": round(d, 4), "dec_GBps": round(b_dec / d / 1e6, 1)}
+        print(n, out["libs"][n], flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
