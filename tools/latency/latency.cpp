@@ -1,0 +1,118 @@
+// latency.cpp -- per-call latency of the C ABI at small messages (the
+// reference's 8 MiB rows, final_results.csv), one process per sync mode:
+//   latency <mode 0..3> [k m bs S iters]
+// mode: 0 default, 1 spin, 2 yield, 3 blocking sync -- set with
+// hipSetDeviceFlags BEFORE any other HIP call (afterwards it is ignored).
+// Prints median/p10/p90 microseconds for: an empty kernel + stream sync,
+// xec_encode + stream sync, xec_encode + event sync, and a captured hipGraph
+// holding the encode + graph sync.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "xec.h"
+
+__global__ void empty_kernel() {}
+
+static void report(const char* name, std::vector<double>& us) {
+  std::sort(us.begin(), us.end());
+  const size_t n = us.size();
+  std::printf("%-28s median %8.2f us  p10 %8.2f  p90 %8.2f\n", name, us[n / 2], us[n / 10],
+              us[n * 9 / 10]);
+}
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));         \
+      return 1;                                                            \
+    }                                                                      \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int mode = argc > 1 ? std::atoi(argv[1]) : 0;
+  const size_t k = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 8;
+  const size_t m = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 4;
+  const size_t bs = argc > 4 ? std::strtoull(argv[4], nullptr, 10) : 1024;
+  const size_t S = argc > 5 ? std::strtoull(argv[5], nullptr, 10) : (8u << 20) / (k * 1024);
+  const int iters = argc > 6 ? std::atoi(argv[6]) : 2000;
+  static const unsigned flags[] = {hipDeviceScheduleAuto, hipDeviceScheduleSpin,
+                                   hipDeviceScheduleYield, hipDeviceScheduleBlockingSync};
+  CK(hipSetDeviceFlags(flags[mode & 3]));
+  if (xec_init(0) != XEC_SUCCESS) return 1;
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  void *d, *p;
+  CK(hipMalloc(&d, S * k * bs));
+  CK(hipMalloc(&p, S * m * bs));
+  CK(hipMemset(d, 0x5a, S * k * bs));
+  CK(hipDeviceSynchronize());
+  std::printf("mode %d  k=%zu m=%zu bs=%zu S=%zu (%zu KiB data)\n", mode, k, m, bs, S,
+              S * k * bs >> 10);
+  using clk = std::chrono::steady_clock;
+  auto us_since = [](clk::time_point t0) {
+    return std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+  };
+  std::vector<double> t;
+  for (int i = 0; i < iters + 50; ++i) {
+    auto t0 = clk::now();
+    empty_kernel<<<1, 64, 0, s>>>();
+    CK(hipStreamSynchronize(s));
+    if (i >= 50) t.push_back(us_since(t0));
+  }
+  report("empty kernel + stream sync", t);
+  t.clear();
+  for (int i = 0; i < iters + 50; ++i) {
+    auto t0 = clk::now();
+    if (xec_encode(d, p, S, bs, k, m, s) != XEC_SUCCESS) return 2;
+    CK(hipStreamSynchronize(s));
+    if (i >= 50) t.push_back(us_since(t0));
+  }
+  report("xec_encode + stream sync", t);
+  t.clear();
+  hipEvent_t ev;
+  CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (int i = 0; i < iters + 50; ++i) {
+    auto t0 = clk::now();
+    if (xec_encode(d, p, S, bs, k, m, s) != XEC_SUCCESS) return 2;
+    CK(hipEventRecord(ev, s));
+    CK(hipEventSynchronize(ev));
+    if (i >= 50) t.push_back(us_since(t0));
+  }
+  report("xec_encode + event sync", t);
+  t.clear();
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  if (xec_encode(d, p, S, bs, k, m, s) != XEC_SUCCESS) return 2;
+  CK(hipStreamEndCapture(s, &g));
+  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  for (int i = 0; i < iters + 50; ++i) {
+    auto t0 = clk::now();
+    CK(hipGraphLaunch(ge, s));
+    CK(hipStreamSynchronize(s));
+    if (i >= 50) t.push_back(us_since(t0));
+  }
+  report("graph(encode) + stream sync", t);
+  t.clear();
+  // device time of the encode alone
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 200; ++i) {
+    CK(hipEventRecord(e0, s));
+    if (xec_encode(d, p, S, bs, k, m, s) != XEC_SUCCESS) return 2;
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    t.push_back(ms * 1e3);
+  }
+  report("encode device time (events)", t);
+  return 0;
+}
