@@ -1,0 +1,29 @@
+"""bench.py's host-side pieces on CPU: the algorithmic byte counts behind
+`value` / `roofline.achieved` and the CPU-baseline leg's
+shape (reference binary when oracle/_ref was built, else the port)."""
+from __future__ import annotations
+
+import bench
+
+
+def test_algorithmic_bytes():
+    # encode reads k, writes m blocks per stripe; single-erasure decode reads
+    # k/m - 1 survivors + 1 parity and writes 1 block
+    assert bench.algorithmic_bytes(256, 16, 1, 1 << 20) == (256 * 17 << 20, 256 * 17 << 20)
+    assert bench.algorithmic_bytes(4096, 16, 4, 65536) == (4096 * 20 * 65536, 4096 * 5 * 65536)
+    assert bench.algorithmic_bytes(1, 4, 1, 4096) == (5 * 4096, 5 * 4096)
+
+
+def test_workloads_match_baseline_configs():
+    k, m, bs, S, desc = bench.WORKLOADS["cfg3"]
+    assert (k, m, bs) == (16, 1, 1 << 20) and "configs[2]" in desc
+    assert bench.WORKLOADS["cfg2"][:4] == (8, 1, 1 << 16, 1024)
+    assert bench.WORKLOADS["cfg4"][:4] == (32, 1, 4096, 65536)
+
+
+def test_cpu_baseline_shape():
+    out = bench.cpu_baseline(8, 1, 1 << 16, 0.2)
+    assert out["kind"] in ("reference", "port")
+    assert out["unit"] == "GB/s" and out["value"] > 0 and out["cores"] >= 1
+    assert out["single_thread"]["value"] > 0
+    assert "stripes" in out["sample"]
