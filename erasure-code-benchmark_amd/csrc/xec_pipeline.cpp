@@ -49,6 +49,31 @@ xec_status sync_all(xec_pipeline* p) {
   return st;
 }
 
+// Error exit: drain what was already queued so no copy touches the caller's
+// buffers after the call returns.
+xec_status fail(xec_pipeline* p, xec_status st) {
+  (void)sync_all(p);
+  return st;
+}
+
+// Copy runs of consecutive blocks of stripe row `bm` (k data bytes) whose
+// bitmap byte is (lost ? 0 : nonzero) -- adjacent blocks merge into one copy.
+template <typename F>
+bool for_runs(const uint8_t* bm, size_t k, bool lost, F&& copy) {
+  size_t i = 0;
+  while (i < k) {
+    if ((bm[i] == 0) != lost) {
+      ++i;
+      continue;
+    }
+    size_t j = i;
+    while (j < k && (bm[j] == 0) == lost) ++j;
+    if (!copy(i, j)) return false;
+    i = j;
+  }
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -104,12 +129,12 @@ xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_pari
     // stream order serialises reuse of this slot behind its previous chunk
     if (hipMemcpyAsync(s.data, src + c0 * k * bs, n * k * bs, hipMemcpyHostToDevice, s.stream) !=
         hipSuccess)
-      return XEC_DEVICE_ERROR;
+      return fail(p, XEC_DEVICE_ERROR);
     xec_status st = xec_encode(s.data, s.parity, n, bs, k, m, s.stream);
-    if (st != XEC_SUCCESS) return st;
+    if (st != XEC_SUCCESS) return fail(p, st);
     if (hipMemcpyAsync(dst + c0 * m * bs, s.parity, n * m * bs, hipMemcpyDeviceToHost, s.stream) !=
         hipSuccess)
-      return XEC_DEVICE_ERROR;
+      return fail(p, XEC_DEVICE_ERROR);
   }
   return sync_all(p);
 }
@@ -135,29 +160,28 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
           break;
         }
     if (!any_lost) continue;  // nothing of this chunk crosses the link
-    if (hipMemcpyAsync(s.data, data + c0 * k * bs, n * k * bs, hipMemcpyHostToDevice, s.stream) !=
-            hipSuccess ||
-        hipMemcpyAsync(s.parity, par + c0 * m * bs, n * m * bs, hipMemcpyHostToDevice, s.stream) !=
-            hipSuccess)
-      return XEC_DEVICE_ERROR;
-    st = xec_decode(s.data, s.parity, n, bs, k, m, h_bitmap + c0 * row, s.bitmap, s.stream);
-    if (st != XEC_SUCCESS) return st;
-    // only the rebuilt blocks go back; adjacent lost blocks merge into one copy
+    // H2D: only the surviving data blocks (a lost block's content is never
+    // read) and the chunk's parity; D2H: only the rebuilt blocks.
     for (size_t c = c0; c < c0 + n; ++c) {
-      size_t i = 0;
-      while (i < k) {
-        if (h_bitmap[c * row + i] != 0) {
-          ++i;
-          continue;
-        }
-        size_t j = i;
-        while (j < k && h_bitmap[c * row + j] == 0) ++j;
-        const size_t off = (c - c0) * k * bs + i * bs;
-        if (hipMemcpyAsync(data + c * k * bs + i * bs, s.data + off, (j - i) * bs,
-                           hipMemcpyDeviceToHost, s.stream) != hipSuccess)
-          return XEC_DEVICE_ERROR;
-        i = j;
-      }
+      const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
+      if (!for_runs(h_bitmap + c * row, k, false, [&](size_t i, size_t j) {
+            return hipMemcpyAsync(s.data + sbase + i * bs, data + base + i * bs, (j - i) * bs,
+                                  hipMemcpyHostToDevice, s.stream) == hipSuccess;
+          }))
+        return fail(p, XEC_DEVICE_ERROR);
+    }
+    if (hipMemcpyAsync(s.parity, par + c0 * m * bs, n * m * bs, hipMemcpyHostToDevice, s.stream) !=
+        hipSuccess)
+      return fail(p, XEC_DEVICE_ERROR);
+    st = xec_decode(s.data, s.parity, n, bs, k, m, h_bitmap + c0 * row, s.bitmap, s.stream);
+    if (st != XEC_SUCCESS) return fail(p, st);
+    for (size_t c = c0; c < c0 + n; ++c) {
+      const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
+      if (!for_runs(h_bitmap + c * row, k, true, [&](size_t i, size_t j) {
+            return hipMemcpyAsync(data + base + i * bs, s.data + sbase + i * bs, (j - i) * bs,
+                                  hipMemcpyDeviceToHost, s.stream) == hipSuccess;
+          }))
+        return fail(p, XEC_DEVICE_ERROR);
     }
   }
   return sync_all(p);
