@@ -1,0 +1,62 @@
+// scan_fuzz.cpp -- host-only fuzz of xec_check_bitmap (csrc/xec_scan.cpp)
+// under AddressSanitizer + UBSan: every bitmap lives in an exact-size heap
+// allocation, so any read past the caller's buffer (the AVX2 row path loads
+// 64-byte windows) is reported.  Verdicts are compared with a direct
+// restatement of require_recovery / is_recoverable (xorec_utils.hpp:144-175).
+//   g++ -std=c++17 -O1 -g -fsanitize=address,undefined -I include \
+//       tests/host/scan_fuzz.cpp erasure-code-benchmark_amd/csrc/xec_scan.cpp
+#include <cstdint>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "xec.h"
+
+static int reference(const uint8_t* bm, size_t S, size_t k, size_t m, int* need) {
+  *need = 0;
+  for (size_t c = 0; c < S; ++c) {
+    const uint8_t* r = bm + c * (k + m);
+    for (size_t i = 0; i < k; ++i)
+      if (!(r[i] & 1u)) *need = 1;
+    for (size_t j = 0; j < m; ++j) {
+      int lost = r[k + j] == 0;
+      for (size_t i = j; i < k; i += m) lost += r[i] == 0;
+      if (lost > 1) return XEC_DECODE_FAILURE;
+    }
+  }
+  return XEC_SUCCESS;
+}
+
+int main() {
+  std::mt19937_64 rng(1896);
+  const size_t ms[] = {1, 2, 3, 4, 5, 8, 16, 32};
+  long cases = 0;
+  for (int trial = 0; trial < 20000; ++trial) {
+    const size_t m = ms[rng() % 8];
+    const size_t k = m * (1 + rng() % (trial % 3 == 0 ? 80 : 12));
+    const size_t S = rng() % 40;
+    const double p_loss = (rng() % 4) * 0.04;
+    const size_t n = S * (k + m);
+    uint8_t* bm = new uint8_t[n ? n : 1];
+    for (size_t i = 0; i < n; ++i) {
+      const double u = (rng() % 10000) / 10000.0;
+      bm[i] = u < p_loss ? 0 : 1;
+      if (trial % 5 == 0 && rng() % 20 == 0) bm[i] = static_cast<uint8_t>(rng() % 256);
+    }
+    int need_ref = 0, need = -1;
+    const int want = reference(bm, S, k, m, &need_ref);
+    const xec_status got = xec_check_bitmap(bm, S, k, m, &need);
+    delete[] bm;
+    if ((int)got != want || (want == XEC_SUCCESS && need != need_ref)) {
+      std::printf("MISMATCH trial %d k=%zu m=%zu S=%zu: got %d/%d want %d/%d\n", trial, k, m, S,
+                  (int)got, need, want, need_ref);
+      return 1;
+    }
+    ++cases;
+  }
+  int need = 0;
+  if (xec_check_bitmap(nullptr, 0, 4, 1, &need) != XEC_SUCCESS || need != 0) return 1;
+  if (xec_check_bitmap(nullptr, 0, 3, 2, &need) != XEC_INVALID_COUNTS) return 1;
+  std::printf("scan_fuzz ok: %ld cases\n", cases);
+  return 0;
+}
