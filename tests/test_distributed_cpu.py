@@ -1,4 +1,4 @@
-"""N>1 path on CPU: gloo, world_size 2 and 3, ragged stripe partitions.
+"""N>1 path on CPU: gloo, world_size 2, 3, 4 and 8, ragged stripe partitions (empty ranks at S < world).
 
 Each rank encodes its own stripe range (oracle encode stands in for the GPU
 kernel: the point here is the partition / scatter / gather / timing logic
@@ -59,7 +59,7 @@ def _worker(rank, world, port, S, k, m, bs, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,S", [(2, 9), (2, 2), (3, 10), (3, 2)])
+@pytest.mark.parametrize("world,S", [(2, 9), (2, 2), (3, 10), (3, 2), (4, 9), (8, 20), (8, 5)])
 def test_partitioned_encode_matches_single_process(world, S):
     k, m, bs = 8, 2, 512
     ctx = mp.get_context("spawn")
