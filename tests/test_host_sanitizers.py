@@ -1,7 +1,8 @@
 """Host code under AddressSanitizer + UBSan (CPU only; GPU sanitizers are not
-available on this pool): the batch recoverability scan of xec_decode,
-fuzzed against a direct restatement of the reference rules with exact-size
-buffers, so an over-read of the caller's bitmap fails the test."""
+available on this pool): the batch recoverability scan of xec_decode, fuzzed
+against a direct restatement of the reference rules with exact-size buffers
+(an over-read of the caller's bitmap fails the test), and the oracle's C
+restatement."""
 from __future__ import annotations
 
 import shutil
@@ -23,3 +24,18 @@ def test_scan_fuzz_asan_ubsan(tmp_path):
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert "scan_fuzz ok" in p.stdout
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_oracle_asan_ubsan(tmp_path):
+    """The oracle itself (the parity checker) under ASan/UBSan: known answers
+    and erase/decode round trips with exact-size buffers."""
+    exe = tmp_path / "oracle_asan"
+    subprocess.run(["gcc", "-std=c11", "-O1", "-g", "-fopenmp", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", f"-I{ROOT / 'oracle'}",
+                    str(ROOT / "tests" / "host" / "oracle_asan.c"),
+                    str(ROOT / "oracle" / "xorec_oracle.c"), "-o", str(exe)],
+                   check=True, capture_output=True)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert "oracle_asan ok" in p.stdout
