@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="cfg3",
+                    help=f"one of {sorted(WORKLOADS)}, or a custom shape k,m,bs,S")
     ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall budget")
@@ -61,6 +62,18 @@ def parse():
                     help="host: xec_decode (reference-shaped: host bitmap scan + H2D copy); "
                          "device: xec_decode_device (bitmap resident, verdict on the device)")
     return ap.parse_args()
+
+
+def workload_shape(name):
+    """A named BASELINE workload, or a custom "k,m,bs,S" (parity-test shapes,
+    sweeps); returns (k, m, bs, S, description)."""
+    if name in WORKLOADS:
+        return WORKLOADS[name]
+    try:
+        k, m, bs, S = (int(x) for x in name.split(","))
+    except ValueError:
+        sys.exit(f"--workload: expected one of {sorted(WORKLOADS)} or k,m,bs,S, got {name!r}")
+    return k, m, bs, S, f"custom: k={k}+{m}, {bs} B shards, {S} stripes per GPU"
 
 
 def algorithmic_bytes(S, k, m, bs):
@@ -229,7 +242,7 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    k, m, bs, S_per, desc = WORKLOADS[args.workload]
+    k, m, bs, S_per, desc = workload_shape(args.workload)
     if args.stripes:
         S_per = args.stripes
     S_total = S_per * world
@@ -332,6 +345,8 @@ def main():
     value = total_bytes / elapsed / 1e9
     if rank == 0:
         traffic, traffic_src = load_traffic(args.workload)
+        if traffic_src and traffic_src.get("encode_algorithmic_bytes_per_launch") != b_enc:
+            traffic, traffic_src = None, None  # profiled at another batch size (--stripes)
         achieved = b_enc / (enc_ms * 1e-3) / 1e9
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
