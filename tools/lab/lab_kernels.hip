@@ -340,6 +340,41 @@ __global__ __launch_bounds__(64) void enc_shfl(const uint8_t* data, uint8_t* par
   }
 }
 
+// Grouped multi-granule tiles: each lane owns UU granules 1 KiB apart (a
+// UU KiB column per wave), members are processed G at a time (G*UU loads in
+// flight), so each member is read as UU KiB contiguous per wave while the
+// register budget stays at full occupancy.
+template <int NM, int G, int UU>
+__global__ __launch_bounds__(64) void enc_group_impl(const uint8_t* data, uint8_t* parity, Geo g) {
+  const uint64_t tpb = g.tpb / UU;  // g.tpb counts 1 KiB tiles
+  const uint64_t t = blockIdx.x;
+  if (t >= g.S * g.m * tpb) return;
+  const uint64_t chunk = t % tpb, cj = t / tpb, j = cj % g.m, c = cj / g.m;
+  const uint64_t stride = g.m * g.bs;
+  const uint8_t* base = data + (c * g.k + j) * g.bs + chunk * UU * 1024 + threadIdx.x * 16;
+  u32x4 acc[UU];
+#pragma unroll
+  for (int u = 0; u < UU; ++u) acc[u] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int r0 = 0; r0 < NM; r0 += G) {
+    u32x4 v[G][UU];
+#pragma unroll
+    for (int r = 0; r < G; ++r)
+#pragma unroll
+      for (int u = 0; u < UU; ++u)
+        v[r][u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + (r0 + r) * stride + u * 1024));
+#pragma unroll
+    for (int r = 0; r < G; ++r)
+#pragma unroll
+      for (int u = 0; u < UU; ++u) acc[u] ^= v[r][u];
+  }
+  uint8_t* dst = parity + (c * g.m + j) * g.bs;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int u = 0; u < UU; ++u)
+    __builtin_amdgcn_raw_buffer_store_b128(acc[u], rs, (uint32_t)(chunk * UU * 1024 + u * 1024 + threadIdx.x * 16), 0, 2);
+}
+
 namespace {
 template <int THREADS>
 Geo geo(uint64_t S, uint64_t bs, uint64_t k, uint64_t m) {
@@ -379,6 +414,15 @@ int launch_seq(const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint
       static_cast<const uint8_t*>(d), static_cast<uint8_t*>(p), g);
   return hipGetLastError() == hipSuccess ? 0 : 6;
 }
+template <int NM, int G, int UU>
+int launch_group(const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint64_t m, hipStream_t s) {
+  if (bs % (UU * 1024)) return 1;
+  Geo g = geo<64>(S, bs, k, m);
+  static_assert(NM % G == 0, "G must divide the member count");
+  enc_group_impl<NM, G, UU><<<(uint32_t)(S * m * (g.tpb / UU)), 64, 0, s>>>(static_cast<const uint8_t*>(d),
+                                                                     static_cast<uint8_t*>(p), g);
+  return hipGetLastError() == hipSuccess ? 0 : 6;
+}
 template <int NM, int THREADS>
 int launch_db(const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint64_t m, uint32_t grid,
               hipStream_t s) {
@@ -400,7 +444,8 @@ const char* lab_variant_name(int v) {
       "Q_wave_u1_w7",      "R_wave_u1_w6",      "S_wave_u1_w4",       "T_wave_u2_w4",
       "U_wave_u2_w5",      "V_wave_u2_w3",      "W_wave_u1_w5",       "X_seq_tpw1",
       "Y_seq_tpw2",        "Z_seq_tpw4",        "AA_lds_stage_256",   "AB_shfl_8x128_64",
-      "AC_xcd_contig_64",  "AD_chunk_fast_64"};
+      "AC_xcd_contig_64",  "AD_chunk_fast_64",  "AE_group_g4_u4",     "AF_group_g2_u4",
+      "AG_group_g8_u2",    "AH_group_g4_u2",    "AI_group_g16_u1"};
   return (v >= 0 && v < (int)(sizeof names / sizeof *names)) ? names[v] : nullptr;
 }
 
@@ -499,6 +544,11 @@ int lab_encode(int v, const void* d, void* p, uint64_t S, uint64_t bs, uint64_t 
     }
     case 28: return launch<16, 64, 2, GLOBAL_NT, 2>(d, p, S, bs, k, m, s);
     case 29: return launch<16, 64, 0, GLOBAL_NT, 2>(d, p, S, bs, k, m, s);
+    case 30: return launch_group<16, 4, 4>(d, p, S, bs, k, m, s);
+    case 31: return launch_group<16, 2, 4>(d, p, S, bs, k, m, s);
+    case 32: return launch_group<16, 8, 2>(d, p, S, bs, k, m, s);
+    case 33: return launch_group<16, 4, 2>(d, p, S, bs, k, m, s);
+    case 34: return launch_group<16, 16, 1>(d, p, S, bs, k, m, s);
   }
   return 1;
 }
