@@ -347,7 +347,23 @@ def main():
         traffic, traffic_src = load_traffic(args.workload)
         if traffic_src and traffic_src.get("encode_algorithmic_bytes_per_launch") != b_enc:
             traffic, traffic_src = None, None  # profiled at another batch size (--stripes)
-        achieved = b_enc / (enc_ms * 1e-3) / 1e9
+        traffic_dec = traffic_src.get("decode_hbm_bytes_per_launch") if traffic_src else None
+
+        def roofline(kernel, b, ms, hbm):
+            achieved = b / (ms * 1e-3) / 1e9
+            r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": hbm,
+                 "kernel": kernel, "algorithmic_bytes_per_launch": b,
+                 "avg_launch_ms": round(ms, 4)}
+            if traffic_src and hbm is not None:
+                r["traffic_source"] = traffic_src.get("source")
+            return r
+
+        # the dominant kernel is the one the step spends longer in (decode at the
+        # BASELINE shapes: in-place writes); both are reported
+        rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic),
+              "decode": roofline("xec::decode_kernel", b_dec, dec_ms, traffic_dec)}
+        dominant = "decode" if dec_ms >= enc_ms else "encode"
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(k, m, bs, args.cpu_seconds)
@@ -372,11 +388,8 @@ def main():
                        "bytes_convention": "algorithmic: enc S(k+m)bs + dec S(k/m+1)bs",
                        "decode_api": "xec_decode_device" if args.decode_api == "device"
                        else "xec_decode"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "kernel": "xec::encode_kernel",
-                         "algorithmic_bytes_per_launch": b_enc,
-                         "avg_launch_ms": round(enc_ms, 4)},
+            "roofline": dict(rl[dominant], dominant_by="avg launch time"),
+            "roofline_by_kernel": rl,
             "cpu_baseline": cpu,
             "encode_ms": round(enc_ms_max, 4),
             "decode_ms": round(dec_ms_max, 4),
@@ -393,8 +406,6 @@ def main():
                     "min_ms": round(min(v), 4), "max_ms": round(max(v), 4)}
                 for n, v in (("encode", enc_list), ("decode", dec_list))},
         }
-        if traffic_src:
-            out["roofline"]["traffic_source"] = traffic_src.get("source")
     else:
         out = None
 
