@@ -8,9 +8,12 @@ over one batch (the reference's timed pair, src/benchmark/abstract_runner.hpp:
 Workload (BASELINE.json configs[2], the config the metric is quoted on):
 k=16 data + m=1 parity, 1 MiB shards, 256 stripes per GPU (4 GiB data,
 256 MiB parity), one lost data block per stripe, (7c) mod k.  Inputs are
-resident in HBM before timing starts.  Two buffer sets alternate so a decode
-never reads parity the preceding encode just left in the 256 MiB Infinity
-Cache: step s encodes set s%2 and decodes set (s+1)%2.
+resident in HBM before timing starts.  Three buffer sets rotate so that no
+kernel reads bytes the kernel before it just wrote (the 256 MiB Infinity
+Cache could serve them): step s encodes set s%3 and decodes set (s+2)%3, so
+the decode of a set and the encode that wrote its parity (and the encode of a
+set and the decode that rewrote its lost blocks) are always two kernels --
+8+ GiB of traffic -- apart.
 
 Multi-GPU: one process per GPU (torchrun); each rank owns a contiguous stripe
 range (xec.partition.stripe_range) -- no collective on the data path; barrier
@@ -33,6 +36,7 @@ sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 SEED = 1896             # RANDOM_SEED, reference src/utils/utils.hpp:26
+NSETS = 3               # resident buffer sets in rotation (module doc)
 
 WORKLOADS = {
     # name: (k, m, bs, stripes per GPU, description)
@@ -250,9 +254,9 @@ def main():
     S = stop - start
     stream = torch.cuda.current_stream()
 
-    # ---- resident inputs: two buffer sets, filled and encoded on the device --
+    # ---- resident inputs: NSETS buffer sets, filled and encoded on the device --
     sets = []
-    for s in range(2):
+    for s in range(NSETS):
         d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
         p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
         seed_base = SEED + start + s * (1 << 40)
@@ -266,8 +270,8 @@ def main():
     bm[np.arange(S), (7 * gidx) % k] = 0
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     d_bm = h_bm.to("cuda")
-    scratch = [torch.empty_like(d_bm) for _ in range(2)]
-    d_status = torch.full((2,), -1, dtype=torch.int32, device="cuda")
+    scratch = [torch.empty_like(d_bm) for _ in range(NSETS)]
+    d_status = torch.full((NSETS,), -1, dtype=torch.int32, device="cuda")
     # The lost block's content on entry to decode is irrelevant (include/xec.h),
     # so the timed loop does not re-erase: every decode still reads k/m-1
     # survivors + parity and rewrites the lost block.  Erasure + rebuild is
@@ -275,17 +279,18 @@ def main():
     torch.cuda.synchronize()
 
     def step(i, ev=None):
-        de, pe, _ = sets[i % 2]
-        dd, pd, _ = sets[(i + 1) % 2]
+        de, pe, _ = sets[i % NSETS]
+        di = (i + NSETS - 1) % NSETS  # the set encoded two kernels ago (module doc)
+        dd, pd, _ = sets[di]
         if ev is not None:
             ev[0].record(stream)
         rc = xec.encode(de, pe, S, bs, k, m, stream)
         if ev is not None:
             ev[1].record(stream)
         if args.decode_api == "device":
-            rc |= xec.decode_device(dd, pd, S, bs, k, m, d_bm, d_status[(i + 1) % 2:], stream)
+            rc |= xec.decode_device(dd, pd, S, bs, k, m, d_bm, d_status[di:], stream)
         else:
-            rc |= xec.decode(dd, pd, S, bs, k, m, h_bm, scratch[(i + 1) % 2], stream)
+            rc |= xec.decode(dd, pd, S, bs, k, m, h_bm, scratch[di], stream)
         if ev is not None:
             ev[2].record(stream)
         return rc
@@ -307,7 +312,7 @@ def main():
         dist.barrier()
     assert rc == 0, "xec call failed inside the timed region"
     if args.decode_api == "device":
-        assert d_status.tolist() == [0, 0], f"device decode verdicts {d_status.tolist()}"
+        assert d_status.tolist() == [0] * NSETS, f"device decode verdicts {d_status.tolist()}"
     elapsed = t1 - t0
     enc_list = [e[0].elapsed_time(e[1]) for e in events]
     dec_list = [e[1].elapsed_time(e[2]) for e in events]

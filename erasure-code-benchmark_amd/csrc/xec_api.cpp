@@ -24,10 +24,23 @@ std::atomic<int> g_unroll{0};
 std::atomic<int> g_max_grid{0};
 std::atomic<int> g_nt{0};
 std::atomic<int> g_threads{0};
+std::atomic<int> g_occupancy{0};  // xec_set_occupancy: waves per SIMD, 0 = no cap
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
 constexpr size_t kAlign = 64;           // XOREC_ALIGNMENT
+
+// LDS to reserve per workgroup so that at most `waves` waves of T-thread
+// workgroups are resident per SIMD: a gfx950 CU has 160 KiB of LDS and 4
+// SIMDs, so 4*waves/(T/64) workgroups fit.  Rounded down to the 512-B
+// allocation granule (7 waves per SIMD comes out as 7.25); 0 = no cap.
+uint32_t lds_for_occupancy(int waves, int threads) {
+  if (waves <= 0 || waves >= 8) return 0;
+  const uint32_t wgs = (uint32_t)(4 * waves) / (uint32_t)(threads / 64);
+  uint32_t b = wgs ? (160u * 1024u) / wgs : 65536u;
+  b &= ~511u;
+  return b > 65536u ? 65536u : b;
+}
 
 // Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
 // non-temporal loads and stores (every byte is touched once), one-wave
@@ -42,6 +55,7 @@ xec::LaunchShape launch_shape(size_t bs) {
   ls.max_grid = g > 0 ? (uint32_t)g : 0u;
   // nt stores address the block with a 32-bit buffer offset (xec_kernels.hip)
   ls.nt = g_nt.load(std::memory_order_relaxed) != 2 && bs <= 0x7fffffffu;
+  ls.lds_bytes = lds_for_occupancy(g_occupancy.load(std::memory_order_relaxed), ls.threads);
   return ls;
 }
 
@@ -127,7 +141,7 @@ xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
-  const xec::Geometry g = xec::make_geometry(S, bs, k, m, xec::LaunchShape{256, 1, 0, false});
+  const xec::Geometry g = xec::make_geometry(S, bs, k, m, xec::LaunchShape{256, 1, 0, false, 0});
   return xec::launch_erase(d_data, d_parity, d_bitmap, g, stream) == hipSuccess ? XEC_SUCCESS
                                                                                : XEC_DEVICE_ERROR;
 }
@@ -171,6 +185,12 @@ xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_
   g_unroll.store(unroll, std::memory_order_relaxed);
   g_max_grid.store(max_grid, std::memory_order_relaxed);
   g_nt.store(cache_policy, std::memory_order_relaxed);
+  return XEC_SUCCESS;
+}
+
+xec_status xec_set_occupancy(int waves_per_simd) {
+  if (waves_per_simd < 0 || waves_per_simd > 8) return XEC_INVALID_SIZE;
+  g_occupancy.store(waves_per_simd, std::memory_order_relaxed);
   return XEC_SUCCESS;
 }
 

@@ -23,6 +23,7 @@ struct LaunchShape {
   int unroll;         // granules per lane per class member: 1 or 2
   uint32_t max_grid;  // 0 = one workgroup per tile, else grid-stride over tiles
   bool nt;            // non-temporal loads/stores
+  uint32_t lds_bytes; // LDS reserved per workgroup to cap residency (0 = none)
 };
 
 inline Geometry make_geometry(uint64_t S, uint64_t bs, uint64_t k, uint64_t m,

@@ -263,16 +263,16 @@ namespace {
 
 template <int NM, int U, bool NT, int T>
 hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t grid,
-                           hipStream_t s) {
-  encode_kernel<NM, U, NT, T><<<grid, T, 0, s>>>(static_cast<const uint8_t*>(d),
+                           uint32_t lds, hipStream_t s) {
+  encode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<const uint8_t*>(d),
                                                  static_cast<uint8_t*>(p), g);
   return hipGetLastError();
 }
 
 template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
-                           uint32_t grid, hipStream_t s) {
-  decode_kernel<NM, U, NT, T><<<grid, T, 0, s>>>(static_cast<uint8_t*>(d),
+                           uint32_t grid, uint32_t lds, hipStream_t s) {
+  decode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<uint8_t*>(d),
                                                  static_cast<const uint8_t*>(p), bm, g);
   return hipGetLastError();
 }
@@ -292,27 +292,29 @@ hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geom
   }
 
 template <int U, bool NT, int T>
-hipError_t enc_nm(const void* d, void* p, const Geometry& g, uint32_t grid, hipStream_t s) {
-  XEC_NM_SWITCH(g.nm, return (launch_encode_t<NM, U, NT, T>(d, p, g, grid, s)))
+hipError_t enc_nm(const void* d, void* p, const Geometry& g, uint32_t grid, uint32_t lds,
+                  hipStream_t s) {
+  XEC_NM_SWITCH(g.nm, return (launch_encode_t<NM, U, NT, T>(d, p, g, grid, lds, s)))
 }
 
 template <int U, bool NT, int T>
 hipError_t dec_nm(void* d, const void* p, const uint8_t* bm, const Geometry& g, uint32_t grid,
-                  hipStream_t s) {
-  XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, grid, s)))
+                  uint32_t lds, hipStream_t s) {
+  XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, grid, lds, s)))
 }
 
 template <bool NT, int T>
 hipError_t enc_u(const void* d, void* p, const Geometry& g, int unroll, uint32_t grid,
-                 hipStream_t s) {
-  return unroll == 2 ? enc_nm<2, NT, T>(d, p, g, grid, s) : enc_nm<1, NT, T>(d, p, g, grid, s);
+                 uint32_t lds, hipStream_t s) {
+  return unroll == 2 ? enc_nm<2, NT, T>(d, p, g, grid, lds, s)
+                     : enc_nm<1, NT, T>(d, p, g, grid, lds, s);
 }
 
 template <bool NT, int T>
 hipError_t dec_u(void* d, const void* p, const uint8_t* bm, const Geometry& g, int unroll,
-                 uint32_t grid, hipStream_t s) {
-  return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, grid, s)
-                     : dec_nm<1, NT, T>(d, p, bm, g, grid, s);
+                 uint32_t grid, uint32_t lds, hipStream_t s) {
+  return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, grid, lds, s)
+                     : dec_nm<1, NT, T>(d, p, bm, g, grid, lds, s);
 }
 
 }  // namespace
@@ -320,11 +322,12 @@ hipError_t dec_u(void* d, const void* p, const uint8_t* bm, const Geometry& g, i
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
                          const LaunchShape& ls, hipStream_t s) {
   const uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
+  const uint32_t lds = ls.lds_bytes;
   if (ls.threads == 256)
-    return ls.nt ? enc_u<true, 256>(d_data, d_parity, g, ls.unroll, grid, s)
-                 : enc_u<false, 256>(d_data, d_parity, g, ls.unroll, grid, s);
-  return ls.nt ? enc_u<true, 64>(d_data, d_parity, g, ls.unroll, grid, s)
-               : enc_u<false, 64>(d_data, d_parity, g, ls.unroll, grid, s);
+    return ls.nt ? enc_u<true, 256>(d_data, d_parity, g, ls.unroll, grid, lds, s)
+                 : enc_u<false, 256>(d_data, d_parity, g, ls.unroll, grid, lds, s);
+  return ls.nt ? enc_u<true, 64>(d_data, d_parity, g, ls.unroll, grid, lds, s)
+               : enc_u<false, 64>(d_data, d_parity, g, ls.unroll, grid, lds, s);
 }
 
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
@@ -332,11 +335,12 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
   Geometry g = g_class;  // decode tiles are (stripe, chunk): see decode_kernel
   g.total_tiles = g.S * g.tiles_per_block;
   const uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
+  const uint32_t lds = ls.lds_bytes;
   if (ls.threads == 256)
-    return ls.nt ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s)
-                 : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s);
-  return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s)
-               : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, s);
+    return ls.nt ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s)
+                 : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s);
+  return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s)
+               : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s);
 }
 
 hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,

@@ -98,6 +98,11 @@ def set_launch(unroll: int = 0, max_grid: int = 0, cache_policy: int = 0,
     return Status(lib().xec_set_launch(unroll, max_grid, cache_policy, block_threads))
 
 
+def set_occupancy(waves_per_simd: int = 0) -> Status:
+    """xec_set_occupancy; cap resident encode/decode waves per SIMD (1..8), 0 = no cap."""
+    return Status(lib().xec_set_occupancy(waves_per_simd))
+
+
 def status_string(st: int) -> str:
     return lib().xec_status_string(int(st)).decode()
 

@@ -140,6 +140,12 @@ xec_status xec_validate_blocks(const void* d_data, size_t nblocks, size_t bs, ui
  *   block_threads workgroup size, 64 (one wave) or 256. */
 xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_threads);
 
+/* Residency cap for tuning sweeps (process-wide, like xec_set_launch): at most
+ * `waves_per_simd` (1..8) encode/decode waves resident per SIMD, enforced by
+ * reserving LDS per workgroup (the kernels use none); 0 = no cap.  Returns
+ * XEC_INVALID_SIZE outside 0..8. */
+xec_status xec_set_occupancy(int waves_per_simd);
+
 /* ---- host-in / host-out pipeline --------------------
  * The MI355X analogue of the reference's GPU-memory / unified-memory variants
  * (src/algorithms/xorec_gpu_ptr_bm.cpp:17-65, xorec_unified_ptr_bm.cpp:15-86,

@@ -160,3 +160,10 @@ def test_set_launch_validation():
     assert xec.set_launch(1, 0, 0, 128) == xec.Status.INVALID_SIZE
     assert xec.set_launch(2, 64, 1, 256) == xec.Status.SUCCESS
     assert xec.set_launch(0, 0, 0, 0) == xec.Status.SUCCESS
+
+
+def test_set_occupancy_validation():
+    assert xec.set_occupancy(-1) == xec.Status.INVALID_SIZE
+    assert xec.set_occupancy(9) == xec.Status.INVALID_SIZE
+    for w in (1, 4, 8, 0):
+        assert xec.set_occupancy(w) == xec.Status.SUCCESS

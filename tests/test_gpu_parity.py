@@ -195,6 +195,24 @@ def test_launch_shapes_bit_exact(gpu, oracle, threads, unroll, max_grid, nt):
         gpu.set_launch(0, 0, 0, 0)
 
 
+@pytest.mark.parametrize("threads", [64, 256])
+@pytest.mark.parametrize("occ", [1, 3, 7])
+def test_occupancy_caps_bit_exact(gpu, oracle, threads, occ):
+    """xec_set_occupancy only reserves LDS per workgroup: results stay bit-exact."""
+    assert gpu.set_launch(0, 0, 0, threads) == gpu.Status.SUCCESS
+    assert gpu.set_occupancy(occ) == gpu.Status.SUCCESS
+    try:
+        for (S, k, m, bs) in [(24, 16, 1, 65536), (40, 32, 4, 4352)]:
+            b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+            bm = np.ones((S, k + m), np.uint8)
+            for c in range(S):
+                oracle.select_lost_blocks(k, m, m, bm[c], 91 + c)
+            erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+    finally:
+        gpu.set_occupancy(0)
+        gpu.set_launch(0, 0, 0, 0)
+
+
 def test_encode_is_linear(gpu):
     """Size-independent property at a full config shape: E(a ^ b) == E(a) ^ E(b)."""
     torch = _torch()

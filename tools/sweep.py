@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--threads", default="64,256")
     ap.add_argument("--grid", default="0,2048,4096")
     ap.add_argument("--nt", default="1,2", help="cache policy: 1 nt, 2 default")
+    ap.add_argument("--occ", default="0", help="waves-per-SIMD caps (xec_set_occupancy), 0 = none")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -73,11 +74,12 @@ def main():
         return [ev[i].elapsed_time(ev[i + 1]) for i in range(args.iters)]
 
     variants = {}
-    for t, u, g, nt in itertools.product(map(int, args.threads.split(",")),
-                                         map(int, args.unroll.split(",")),
-                                         map(int, args.grid.split(",")),
-                                         map(int, args.nt.split(","))):
-        variants[f"t{t}_u{u}_g{g}_nt{nt}"] = (t, u, g, nt)
+    for t, u, g, nt, o in itertools.product(map(int, args.threads.split(",")),
+                                            map(int, args.unroll.split(",")),
+                                            map(int, args.grid.split(",")),
+                                            map(int, args.nt.split(",")),
+                                            map(int, args.occ.split(","))):
+        variants[f"t{t}_u{u}_g{g}_nt{nt}" + (f"_o{o}" if o else "")] = (t, u, g, nt, o)
 
     # references on the same byte volume
     big = sets[0][0]
@@ -89,13 +91,15 @@ def main():
     results["torch_copy"] = {"GBps": []}
     results["torch_xor2"] = {"GBps": []}
     for _ in range(args.rounds):
-        for name, (t, u, g, nt) in variants.items():
+        for name, (t, u, g, nt, o) in variants.items():
             assert xec.set_launch(u, g, nt, t) == 0
+            assert xec.set_occupancy(o) == 0
             results[name]["enc"] += time_it(
                 lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
             results[name]["dec"] += time_it(
                 lambda i: xec.decode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, h_bm, scratch, s))
         xec.set_launch(0, 0, 0, 0)
+        xec.set_occupancy(0)
         t = time_it(lambda i: copy_dst.copy_(big))
         results["torch_copy"]["GBps"] += [2 * big.numel() / (x * 1e-3) / 1e9 for x in t]
         t = time_it(lambda i: torch.bitwise_xor(big[:half // 2 * 2][:half], big[half:half * 2],
