@@ -24,7 +24,7 @@ std::atomic<int> g_unroll{0};
 std::atomic<int> g_max_grid{0};
 std::atomic<int> g_nt{0};
 std::atomic<int> g_threads{0};
-std::atomic<int> g_occupancy{0};  // xec_set_occupancy: waves per SIMD, 0 = no cap
+std::atomic<int> g_occupancy{0};  // xec_set_occupancy: waves per SIMD, 0 = automatic
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
@@ -42,10 +42,27 @@ uint32_t lds_for_occupancy(int waves, int threads) {
   return b > 65536u ? 65536u : b;
 }
 
+// Resident waves per SIMD that measured fastest for the default shape (one
+// wave per workgroup, one granule per lane), by class member count k/m
+// (tools/sweep.py --occ; profiles/r01i, r01j: two devices, encode and decode,
+// k=4..32).  Each wave has k/m KiB of loads in flight; the best residency keeps
+// about 32 KiB in flight per SIMD (16 KiB at k/m = 4) -- 8 waves of 16 KiB at
+// k/m = 16 crowd HBM with 4x the requests and ran 3 % (encode) to 6 % (decode)
+// slower.  0 = no cap (8 per SIMD).
+int auto_occupancy(uint64_t nm) {
+  switch (nm) {
+    case 4: case 8: return 4;
+    case 16: return 2;
+    case 32: return 1;
+    default: return 0;
+  }
+}
+
 // Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
 // non-temporal loads and stores (every byte is touched once), one-wave
-// workgroups with one 1 KiB tile each, one workgroup per tile.
-xec::LaunchShape launch_shape(size_t bs) {
+// workgroups with one 1 KiB tile each, one workgroup per tile, residency
+// capped per member count (auto_occupancy).
+xec::LaunchShape launch_shape(size_t bs, size_t nm) {
   xec::LaunchShape ls;
   const int t = g_threads.load(std::memory_order_relaxed);
   ls.threads = t == 256 ? 256 : 64;
@@ -55,7 +72,9 @@ xec::LaunchShape launch_shape(size_t bs) {
   ls.max_grid = g > 0 ? (uint32_t)g : 0u;
   // nt stores address the block with a 32-bit buffer offset (xec_kernels.hip)
   ls.nt = g_nt.load(std::memory_order_relaxed) != 2 && bs <= 0x7fffffffu;
-  ls.lds_bytes = lds_for_occupancy(g_occupancy.load(std::memory_order_relaxed), ls.threads);
+  int w = g_occupancy.load(std::memory_order_relaxed);
+  if (w == 0) w = (ls.threads == 64 && ls.unroll == 1) ? auto_occupancy(nm) : 0;
+  ls.lds_bytes = lds_for_occupancy(w, ls.threads);
   return ls;
 }
 
@@ -89,7 +108,7 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
-  const xec::LaunchShape ls = launch_shape(bs);
+  const xec::LaunchShape ls = launch_shape(bs, k / m);
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   return xec::launch_encode(d_data, d_parity, g, ls, stream) == hipSuccess ? XEC_SUCCESS
                                                                            : XEC_DEVICE_ERROR;
@@ -108,7 +127,7 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   if (hipMemcpyAsync(d_bitmap, h_bitmap, S * (k + m), hipMemcpyHostToDevice, stream) !=
       hipSuccess)
     return XEC_DEVICE_ERROR;
-  const xec::LaunchShape ls = launch_shape(bs);
+  const xec::LaunchShape ls = launch_shape(bs, k / m);
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
              ? XEC_SUCCESS
@@ -126,7 +145,7 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
   if (hipMemsetAsync(d_status, 0, sizeof(int32_t), stream) != hipSuccess) return XEC_DEVICE_ERROR;
   if (S == 0) return XEC_SUCCESS;
   if (d_bitmap == nullptr) return XEC_INVALID_ALIGNMENT;
-  const xec::LaunchShape ls = launch_shape(bs);
+  const xec::LaunchShape ls = launch_shape(bs, k / m);
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   if (xec::launch_check(d_bitmap, g, d_status, stream) != hipSuccess) return XEC_DEVICE_ERROR;
   g.gate = d_status;

@@ -99,7 +99,8 @@ def set_launch(unroll: int = 0, max_grid: int = 0, cache_policy: int = 0,
 
 
 def set_occupancy(waves_per_simd: int = 0) -> Status:
-    """xec_set_occupancy; cap resident encode/decode waves per SIMD (1..8), 0 = no cap."""
+    """xec_set_occupancy; resident encode/decode waves per SIMD (1..8, 8 = no cap),
+    0 = automatic (measured per member count; the default)."""
     return Status(lib().xec_set_occupancy(waves_per_simd))
 
 

@@ -140,10 +140,14 @@ xec_status xec_validate_blocks(const void* d_data, size_t nblocks, size_t bs, ui
  *   block_threads workgroup size, 64 (one wave) or 256. */
 xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_threads);
 
-/* Residency cap for tuning sweeps (process-wide, like xec_set_launch): at most
- * `waves_per_simd` (1..8) encode/decode waves resident per SIMD, enforced by
- * reserving LDS per workgroup (the kernels use none); 0 = no cap.  Returns
- * XEC_INVALID_SIZE outside 0..8. */
+/* Residency of the encode/decode kernels (process-wide, like xec_set_launch):
+ * at most `waves_per_simd` (1..8; 8 = no cap) waves resident per SIMD,
+ * enforced by reserving LDS per workgroup (the kernels use none).
+ * 0 = automatic (the default): the cap measured fastest for the member count
+ * k/m at the default launch shape -- 1 at k/m = 32, 2 at 16, 4 at 4 and 8,
+ * none otherwise.  The reserved LDS keeps other kernels' LDS
+ * users off those CUs while a launch runs.  Returns XEC_INVALID_SIZE outside
+ * 0..8. */
 xec_status xec_set_occupancy(int waves_per_simd);
 
 /* ---- host-in / host-out pipeline --------------------

@@ -196,7 +196,7 @@ def test_launch_shapes_bit_exact(gpu, oracle, threads, unroll, max_grid, nt):
 
 
 @pytest.mark.parametrize("threads", [64, 256])
-@pytest.mark.parametrize("occ", [1, 3, 7])
+@pytest.mark.parametrize("occ", [1, 3, 7, 8])
 def test_occupancy_caps_bit_exact(gpu, oracle, threads, occ):
     """xec_set_occupancy only reserves LDS per workgroup: results stay bit-exact."""
     assert gpu.set_launch(0, 0, 0, threads) == gpu.Status.SUCCESS

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--threads", default="64,256")
     ap.add_argument("--grid", default="0,2048,4096")
     ap.add_argument("--nt", default="1,2", help="cache policy: 1 nt, 2 default")
-    ap.add_argument("--occ", default="0", help="waves-per-SIMD caps (xec_set_occupancy), 0 = none")
+    ap.add_argument("--occ", default="0", help="waves-per-SIMD caps (xec_set_occupancy): 0 = automatic, 8 = none")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
