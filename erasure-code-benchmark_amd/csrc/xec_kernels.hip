@@ -105,6 +105,12 @@ __device__ __forceinline__ void xor_members(const uint8_t* base, uint64_t stride
 #pragma unroll
         for (int u = 0; u < U; ++u) v[r][u] = ld16<NT>(src + u * kStep);
       }
+      // At 32+ members the compiler otherwise keeps a rolling window of ~11
+      // loads in flight; with residency capped at one wave per SIMD
+      // (xec_api.cpp auto_occupancy) all 32 in flight measured +4-6 %
+      // (decode at config 4, encode at 32+1 x 64 KiB; tools/ab,
+      // profiles/r01m).  At 16 members the window is faster (-2 %).
+      if constexpr (NM >= 32) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         u32x4 acc = v[0][u];

@@ -38,6 +38,9 @@ def main():
                     help="bench.py workload name, or k,m,bs,S")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--occ", default="",
+                    help="comma list of xec_set_occupancy values to cross with --libs "
+                         "(0 = automatic, 8 = none); default: each lib's default only")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -48,7 +51,12 @@ def main():
 
     torch.cuda.set_device(0)
     assert xec.init(0) == 0
-    libs = {n: load(n) for n in args.libs.split(",")}
+    loaded = {n: load(n) for n in args.libs.split(",")}
+    occs = [int(x) for x in args.occ.split(",")] if args.occ else [None]
+    libs = {}
+    for n, L in loaded.items():
+        for o in occs:
+            libs[n if o is None else f"{n}@o{o}"] = (L, o)
     if args.workload in WORKLOADS:
         k, m, bs, S, _ = WORKLOADS[args.workload]
     else:
@@ -69,7 +77,13 @@ def main():
 
     # every build must produce the same parity and the same rebuilt data
     ref = None
-    for n, L in libs.items():
+    def use(L, o):
+        if o is not None:
+            assert L.xec_set_occupancy(o) == 0
+        return L
+
+    for n, (L, o) in libs.items():
+        use(L, o)
         d, p = sets[0]
         assert L.xec_encode(d.data_ptr(), p.data_ptr(), S, bs, k, m, sh) == 0
         assert L.xec_decode(d.data_ptr(), p.data_ptr(), S, bs, k, m, h_bm.data_ptr(),
@@ -93,7 +107,8 @@ def main():
 
     res = {n: {"enc": [], "dec": []} for n in libs}
     for _ in range(args.rounds):
-        for n, L in libs.items():
+        for n, (L, o) in libs.items():
+            use(L, o)
             res[n]["enc"] += run(lambda i, L=L: L.xec_encode(
                 sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
             res[n]["dec"] += run(lambda i, L=L: L.xec_decode(
