@@ -87,6 +87,23 @@ def algorithmic_bytes(S, k, m, bs):
     return S * (k + m) * bs, S * (k // m + 1) * bs
 
 
+def erasure_pattern(np, S, k, m, lost=1, start=0):
+    """Bitmap (S, k+m) of the bench's erasures: one lost data block per stripe at
+    (7c) mod k over the global stripe index c; with lost > 1
+    (tools), `lost` data blocks per stripe, each in its own parity class
+    (class (c+q) mod m, member (7c+q) mod k/m), so every stripe stays
+    recoverable (is_recoverable, xorec_utils.hpp:160-175)."""
+    c = np.arange(start, start + S)
+    bm = np.ones((S, k + m), dtype=np.uint8)
+    if lost == 1:
+        bm[np.arange(S), (7 * c) % k] = 0
+        return bm
+    assert 1 <= lost <= m, "lost must be 1..m"
+    for q in range(lost):
+        bm[np.arange(S), (c + q) % m + m * ((7 * c + q) % (k // m))] = 0
+    return bm
+
+
 def load_traffic(workload):
     """PMC-measured HBM bytes per encode launch, from profiles/ (tools/pmc_traffic.py)."""
     f = ROOT / "profiles" / f"traffic_{workload}.json"
@@ -265,9 +282,7 @@ def main():
         sets.append((d, p, seed_base))
     # single erasure per stripe, (7c) mod k over the GLOBAL stripe index
     import numpy as np
-    gidx = np.arange(start, stop)
-    bm = np.ones((S, k + m), dtype=np.uint8)
-    bm[np.arange(S), (7 * gidx) % k] = 0
+    bm = erasure_pattern(np, S, k, m, 1, start)
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     d_bm = h_bm.to("cuda")
     scratch = [torch.empty_like(d_bm) for _ in range(NSETS)]

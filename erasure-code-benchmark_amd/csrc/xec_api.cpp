@@ -13,6 +13,7 @@
 
 #include <atomic>
 
+#include "xec_internal.h"
 #include "xec_kernels.h"
 
 namespace {
@@ -58,11 +59,23 @@ int auto_occupancy(uint64_t nm) {
   }
 }
 
+// Decode does one class reduction per lost data block of its stripe, one after
+// the other, so its work per tile is k/m x (lost blocks per stripe) loads.  At
+// one erasure per stripe that is the encode table above; with several
+// (tools/sweep.py --lost, profiles/r01p: 16+2, 16+4, 16+8, 32+8, 8+2 at 2..8
+// erasures per stripe) 2 waves per SIMD measured best from 8 loads per tile
+// up (+3 to +15 % over the single-erasure choice), 4 from 4.
+int decode_auto_occupancy(uint64_t nm, uint64_t lost_data, uint64_t S) {
+  if (lost_data <= S) return auto_occupancy(nm);
+  const uint64_t work = nm * ((lost_data + S - 1) / S);
+  return work >= 8 ? 2 : work >= 4 ? 4 : 0;
+}
+
 // Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
 // non-temporal loads and stores (every byte is touched once), one-wave
 // workgroups with one 1 KiB tile each, one workgroup per tile, residency
 // capped per member count (auto_occupancy).
-xec::LaunchShape launch_shape(size_t bs, size_t nm) {
+xec::LaunchShape launch_shape(size_t bs, int auto_w) {
   xec::LaunchShape ls;
   const int t = g_threads.load(std::memory_order_relaxed);
   ls.threads = t == 256 ? 256 : 64;
@@ -73,7 +86,7 @@ xec::LaunchShape launch_shape(size_t bs, size_t nm) {
   // nt stores address the block with a 32-bit buffer offset (xec_kernels.hip)
   ls.nt = g_nt.load(std::memory_order_relaxed) != 2 && bs <= 0x7fffffffu;
   int w = g_occupancy.load(std::memory_order_relaxed);
-  if (w == 0) w = (ls.threads == 64 && ls.unroll == 1) ? auto_occupancy(nm) : 0;
+  if (w == 0) w = (ls.threads == 64 && ls.unroll == 1) ? auto_w : 0;
   ls.lds_bytes = lds_for_occupancy(w, ls.threads);
   return ls;
 }
@@ -91,7 +104,7 @@ xec_status xec_check_args(const void* data, const void* parity, size_t bs, size_
   return XEC_SUCCESS;
 }
 
-// xec_check_bitmap lives in xec_scan.cpp (host-only, AVX2 where available).
+// xec_check_bitmap / xec_scan_bitmap live in xec_scan.cpp (host-only, AVX2 where available).
 
 xec_status xec_init(int device_id) {
   int count = 0;
@@ -108,7 +121,7 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
-  const xec::LaunchShape ls = launch_shape(bs, k / m);
+  const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   return xec::launch_encode(d_data, d_parity, g, ls, stream) == hipSuccess ? XEC_SUCCESS
                                                                            : XEC_DEVICE_ERROR;
@@ -121,13 +134,14 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
   int needs = 0;
-  st = xec_check_bitmap(h_bitmap, S, k, m, &needs);
+  uint64_t lost = 0;
+  st = xec_scan_bitmap(h_bitmap, S, k, m, &needs, &lost);
   if (st != XEC_SUCCESS) return st;
   if (!needs) return XEC_SUCCESS;
   if (hipMemcpyAsync(d_bitmap, h_bitmap, S * (k + m), hipMemcpyHostToDevice, stream) !=
       hipSuccess)
     return XEC_DEVICE_ERROR;
-  const xec::LaunchShape ls = launch_shape(bs, k / m);
+  const xec::LaunchShape ls = launch_shape(bs, decode_auto_occupancy(k / m, lost, S));
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
              ? XEC_SUCCESS
@@ -145,7 +159,7 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
   if (hipMemsetAsync(d_status, 0, sizeof(int32_t), stream) != hipSuccess) return XEC_DEVICE_ERROR;
   if (S == 0) return XEC_SUCCESS;
   if (d_bitmap == nullptr) return XEC_INVALID_ALIGNMENT;
-  const xec::LaunchShape ls = launch_shape(bs, k / m);
+  const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   if (xec::launch_check(d_bitmap, g, d_status, stream) != hipSuccess) return XEC_DEVICE_ERROR;
   g.gate = d_status;

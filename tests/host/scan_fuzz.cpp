@@ -2,7 +2,8 @@
 // under AddressSanitizer + UBSan: every bitmap lives in an exact-size heap
 // allocation, so any read past the caller's buffer (the AVX2 row path loads
 // 64-byte windows) is reported.  Verdicts are compared with a direct
-// restatement of require_recovery / is_recoverable (xorec_utils.hpp:144-175).
+// restatement of require_recovery / is_recoverable (xorec_utils.hpp:144-175);
+// xec_scan_bitmap's lost-data-block count is checked against a direct count.
 //   g++ -std=c++17 -O1 -g -fsanitize=address,undefined -I include \
 //       tests/host/scan_fuzz.cpp erasure-code-benchmark_amd/csrc/xec_scan.cpp
 #include <cstdint>
@@ -11,6 +12,7 @@
 #include <vector>
 
 #include "xec.h"
+#include "../../erasure-code-benchmark_amd/csrc/xec_internal.h"
 
 static int reference(const uint8_t* bm, size_t S, size_t k, size_t m, int* need) {
   *need = 0;
@@ -43,10 +45,19 @@ int main() {
       bm[i] = u < p_loss ? 0 : 1;
       if (trial % 5 == 0 && rng() % 20 == 0) bm[i] = static_cast<uint8_t>(rng() % 256);
     }
-    int need_ref = 0, need = -1;
+    int need_ref = 0, need = -1, need2 = -1;
     const int want = reference(bm, S, k, m, &need_ref);
     const xec_status got = xec_check_bitmap(bm, S, k, m, &need);
+    uint64_t lost = ~0ull, lost_ref = 0;
+    const xec_status got2 = xec_scan_bitmap(bm, S, k, m, &need2, &lost);
+    for (size_t c = 0; c < S; ++c)
+      for (size_t i = 0; i < k; ++i) lost_ref += bm[c * (k + m) + i] == 0;
     delete[] bm;
+    if (got2 != got || (want == XEC_SUCCESS && (need2 != need_ref || lost != lost_ref))) {
+      std::printf("SCAN MISMATCH trial %d k=%zu m=%zu S=%zu: lost %llu want %llu\n", trial, k, m,
+                  S, (unsigned long long)lost, (unsigned long long)lost_ref);
+      return 1;
+    }
     if ((int)got != want || (want == XEC_SUCCESS && need != need_ref)) {
       std::printf("MISMATCH trial %d k=%zu m=%zu S=%zu: got %d/%d want %d/%d\n", trial, k, m, S,
                   (int)got, need, want, need_ref);

@@ -18,7 +18,7 @@ ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 
-from bench import WORKLOADS, algorithmic_bytes  # noqa: E402
+from bench import WORKLOADS, algorithmic_bytes, erasure_pattern  # noqa: E402
 
 
 def load(name: str):
@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--occ", default="",
                     help="comma list of xec_set_occupancy values to cross with --libs "
                          "(0 = automatic, 8 = none); default: each lib's default only")
+    ap.add_argument("--lost", type=int, default=1, help="lost data blocks per stripe (1..m)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -69,11 +70,11 @@ def main():
         p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
         assert xec.fill_splitmix64(d, S, k * bs, 1896 + 7919 * i, s) == 0
         sets.append((d, p))
-    bm = np.ones((S, k + m), np.uint8)
-    bm[np.arange(S), (7 * np.arange(S)) % k] = 0
+    bm = erasure_pattern(np, S, k, m, args.lost)
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     scratch = h_bm.to("cuda")
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
+    b_dec *= args.lost
 
     # every build must produce the same parity and the same rebuilt data
     ref = None
@@ -114,7 +115,8 @@ def main():
             res[n]["dec"] += run(lambda i, L=L: L.xec_decode(
                 sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(), S, bs, k, m,
                 h_bm.data_ptr(), scratch.data_ptr(), sh))
-    out = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S, "libs": {}}
+    out = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S, "lost": args.lost,
+           "libs": {}}
     for n, r in res.items():
         e, d = statistics.median(r["enc"]), statistics.median(r["dec"])
         out["libs"][n] = {"enc_ms_med": round(e, 4), "enc_GBps": round(b_enc / e / 1e6, 1),

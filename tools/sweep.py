@@ -21,7 +21,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 sys.path.insert(0, str(ROOT))
 
-from bench import WORKLOADS, algorithmic_bytes  # noqa: E402
+from bench import WORKLOADS, algorithmic_bytes, erasure_pattern  # noqa: E402
 
 
 def main():
@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--grid", default="0,2048,4096")
     ap.add_argument("--nt", default="1,2", help="cache policy: 1 nt, 2 default")
     ap.add_argument("--occ", default="0", help="waves-per-SIMD caps (xec_set_occupancy): 0 = automatic, 8 = none")
+    ap.add_argument("--lost", type=int, default=1,
+                    help="lost data blocks per stripe (<= m, one per parity class)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -57,11 +59,11 @@ def main():
         assert xec.fill_splitmix64(d, S, k * bs, 1896 + i * 100000, s) == 0
         assert xec.encode(d, p, S, bs, k, m, s) == 0
         sets.append((d, p))
-    bm = np.ones((S, k + m), np.uint8)
-    bm[np.arange(S), (7 * np.arange(S)) % k] = 0  # one lost data block per stripe
+    bm = erasure_pattern(np, S, k, m, args.lost)  # bench.py: one per class per stripe
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     scratch = h_bm.to("cuda")
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
+    b_dec *= args.lost  # each lost block: k/m - 1 survivors + parity read, 1 block written
 
     def time_it(fn):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
@@ -106,7 +108,7 @@ def main():
                                                 out=xor_out))
         results["torch_xor2"]["GBps"] += [3 * half / (x * 1e-3) / 1e9 for x in t]
 
-    summary = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S,
+    summary = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S, "lost": args.lost,
                "b_enc": b_enc, "b_dec": b_dec, "variants": {}}
     for name, r in results.items():
         if "enc" in r:
