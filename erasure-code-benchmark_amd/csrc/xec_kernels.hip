@@ -51,17 +51,28 @@ __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
   else *q = v;
 }
 
+// Cache policy of the result stores of the NT kernels (gfx950 buffer aux bits:
+// sc0 = 1, nt = 2, sc1 = 16).  Encode stores parity `nt`.  Decode stores the
+// rebuilt block `sc1`, which does not keep the line in the XCD's L2
+// (MI355X_MICROARCH.md, stores of each flavour): the rebuilt line shares its
+// L2 set with the same column of the blocks the tile is reading, and an
+// in-place nt line left dirty there measured 3-6 % slower (config 3, config
+// 2, 16+4, 32+1 x 64 KiB on two devices; tools/ab/patches/store_policy.py,
+// profiles/r01r, r01s); for encode sc1 was -2..+3 %, so it stays nt.
+constexpr int kEncodeStoreAux = 2;   // nt
+constexpr int kDecodeStoreAux = 16;  // sc1
+
 // Store 16 bytes at block + off.  With NT the store is a buffer store whose
-// cache policy is an explicit operand (aux 2 = nt): hipcc (ROCm 7.2) silently
-// drops the !nontemporal of __builtin_nontemporal_store in the unrolled
-// reduction below (the emitted global_store has no `nt`), which measured 5 %
-// slower.  tests/test_isa.py checks every NT kernel's stores carry nt.
-template <bool NT>
+// cache policy is an explicit operand (AUX): hipcc (ROCm 7.2) silently drops
+// the !nontemporal of __builtin_nontemporal_store in the unrolled reduction
+// below (the emitted global_store has no `nt`), which measured 5 % slower.
+// tests/test_isa.py checks every NT kernel's stores carry their policy.
+template <bool NT, int AUX>
 __device__ __forceinline__ void st16_block(uint8_t* block, uint64_t off, u32x4 v) {
   if constexpr (NT) {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(block, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)off, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)off, 0, AUX);
   } else {
     st16<false>(block + off, v);
   }
@@ -87,7 +98,8 @@ __device__ __forceinline__ TileCoord tile_coord(uint64_t t, const Geometry& g) {
 // `subst`, whose bytes come from `sub` instead (decode: the class parity).
 // `off` = this lane's byte offset of granule 0 in the block; granule u is
 // off + u*T*16 and takes part only while inside the block (ragged tiles).
-template <int NM, int U, bool NT, int T>
+// SAUX = cache policy of the NT result store (kEncodeStoreAux / kDecodeStoreAux).
+template <int NM, int U, bool NT, int T, int SAUX>
 __device__ __forceinline__ void xor_members(const uint8_t* base, uint64_t stride,
                                             const uint8_t* sub, int subst, uint8_t* dst,
                                             uint64_t off, uint64_t bs, uint32_t nm_rt) {
@@ -116,7 +128,7 @@ __device__ __forceinline__ void xor_members(const uint8_t* base, uint64_t stride
         u32x4 acc = v[0][u];
 #pragma unroll
         for (int r = 1; r < NM; ++r) acc ^= v[r][u];
-        st16_block<NT>(dst, off + u * kStep, acc);
+        st16_block<NT, SAUX>(dst, off + u * kStep, acc);
       }
       return;
     }
@@ -141,7 +153,7 @@ __device__ __forceinline__ void xor_members(const uint8_t* base, uint64_t stride
       for (int q = 0; q < 8; ++q) acc ^= v[q];
     }
     for (; r < nm; ++r) acc ^= ld16<NT>(((int)r == subst ? sub : base + (uint64_t)r * stride) + o);
-    st16_block<NT>(dst, o, acc);
+    st16_block<NT, SAUX>(dst, o, acc);
   }
 }
 
@@ -156,7 +168,8 @@ __global__ __launch_bounds__(T) void encode_kernel(const uint8_t* __restrict__ d
     const uint8_t* base = data + (tc.c * g.k + tc.j) * g.bs;
     uint8_t* dst = parity + (tc.c * g.m + tc.j) * g.bs;
     const uint64_t off = (tc.chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
-    xor_members<NM, U, NT, T>(base, g.m * g.bs, nullptr, -1, dst, off, g.bs, (uint32_t)g.nm);
+    xor_members<NM, U, NT, T, kEncodeStoreAux>(base, g.m * g.bs, nullptr, -1, dst, off, g.bs,
+                                               (uint32_t)g.nm);
   }
 }
 
@@ -200,8 +213,9 @@ __global__ __launch_bounds__(T) void decode_kernel(uint8_t* data, const uint8_t*
         z &= z - 1;
         const uint32_t j = i % m, r = i / m;  // class and member of lost block i
         uint8_t* base = sdata + (uint64_t)j * g.bs;
-        xor_members<NM, U, NT, T>(base, stride, spar + (uint64_t)j * g.bs, (int)r,
-                                  base + (uint64_t)r * stride, off, g.bs, nm);
+        xor_members<NM, U, NT, T, kDecodeStoreAux>(base, stride, spar + (uint64_t)j * g.bs,
+                                                   (int)r, base + (uint64_t)r * stride, off,
+                                                   g.bs, nm);
       }
     }
   }

@@ -1,8 +1,9 @@
 """ISA-level invariants of the gfx950 kernels (CPU only: hipcc cross-compiles).
 
-* every load and store of a non-temporal (NT=true) encode/decode instantiation
-  carries the `nt` cache policy -- hipcc has been seen to drop it silently
-  (xec_kernels.hip, st16_block), which cost 5 % of bandwidth;
+* every load of a non-temporal (NT=true) encode/decode instantiation carries
+  `nt` and every result store its kernel's policy (encode `nt`, decode `sc1`)
+  -- hipcc has been seen to drop `nt` silently (xec_kernels.hip, st16_block),
+  which cost 5 % of bandwidth;
 * the benchmark-shape kernels' registers admit the residency the launch asks
   for by default (auto_occupancy in csrc/xec_api.cpp), and the 32-member
   kernels issue all their loads before the first wait.
@@ -41,14 +42,23 @@ def _nt(name: str) -> bool:
     return re.search(r"ELb1E", name) is not None
 
 
-def test_nt_kernels_use_nt_everywhere(kernels):
+def test_nt_kernels_carry_their_cache_policy(kernels):
+    """Every load of an NT kernel is `nt`; its result stores carry the policy
+    chosen per kernel (xec_kernels.hip kEncodeStoreAux / kDecodeStoreAux):
+    encode `nt`, decode `sc1` (not kept in L2)."""
     for name, k in kernels.items():
         if not _nt(name):
             continue
-        mem = re.findall(r"^\s*((?:global|buffer)_(?:load|store)_dwordx4[^\n]*)", k["body"], re.M)
-        assert mem, name
-        missing = [i for i in mem if not re.search(r"\bnt\b", i)]
+        loads = re.findall(r"^\s*((?:global|buffer)_load_dwordx4[^\n]*)", k["body"], re.M)
+        stores = re.findall(r"^\s*((?:global|buffer)_store_dwordx4[^\n]*)", k["body"], re.M)
+        assert loads and stores, name
+        missing = [i for i in loads if not re.search(r"\bnt\b", i)]
         assert not missing, f"{name}: {missing[:3]}"
+        want = r"\bsc1\b" if "decode_kernel" in name else r"\bnt\b"
+        wrong = [i for i in stores if not re.search(want, i)]
+        assert not wrong, f"{name}: {wrong[:3]}"
+        if "decode_kernel" in name:
+            assert not [i for i in stores if re.search(r"\bnt\b", i)], name
 
 
 # member count -> resident waves per SIMD the launch asks for by default
