@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--decode", action="store_true", help="time the decode diagnostics")
     ap.add_argument("--ceiling", action="store_true", help="time read/write/copy ceilings")
+    ap.add_argument("--occ", default="0", help="--ceiling: waves-per-SIMD caps (0 = none), "
+                                               "crossed with the product encode's own setting")
     args = ap.parse_args()
 
     import torch
@@ -192,18 +194,38 @@ def ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):
         torch.cuda.synchronize()
         return [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.iters)]
 
-    bytes_ = {"read_only_16way": S * k * bs, "write_only": S * bs, "copy": 2 * S * bs,
-              "product_encode": S * (k + m) * bs}
+    L.lab_set_ceiling_lds.argtypes = [ctypes.c_uint32]
+    occs = [int(x) for x in args.occ.split(",")]
+
+    def lds(w):  # as csrc/xec_api.cpp lds_for_occupancy for one-wave workgroups
+        return 0 if w <= 0 or w >= 8 else ((160 * 1024) // (4 * w)) & ~511
+
+    base = {"read_only_16way": S * k * bs, "write_only": S * bs, "copy": 2 * S * bs}
+    bytes_, res = {}, {}
+    for w in occs:
+        for n, b in base.items():
+            bytes_[f"{n}_o{w}"] = b
+        bytes_[f"product_encode_occ{w}"] = S * (k + m) * bs
     res = {n: [] for n in bytes_}
     for _ in range(args.rounds):
-        res["product_encode"] += run(lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
-        for mode, n in enumerate(["read_only_16way", "write_only", "copy"]):
-            res[n] += run(lambda i, mode=mode: L.lab_ceiling(mode, sets[i % 2][0].data_ptr(),
-                                                              sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
+        for w in occs:
+            assert xec.set_occupancy(w) == 0
+            res[f"product_encode_occ{w}"] += run(
+                lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
+            L.lab_set_ceiling_lds(lds(w))
+            for mode, n in enumerate(base):
+                res[f"{n}_o{w}"] += run(lambda i, mode=mode: L.lab_ceiling(
+                    mode, sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
+    xec.set_occupancy(0)
+    L.lab_set_ceiling_lds(0)
+    out = {}
     for n, ts in res.items():
         med = statistics.median(ts)
-        print(f"{n:20s} ms_med {med:.4f}  GBps_med {bytes_[n] / (med * 1e-3) / 1e9:.1f}  "
-              f"GBps_best {bytes_[n] / (min(ts) * 1e-3) / 1e9:.1f}")
+        out[n] = {"ms_med": round(med, 4), "GBps_med": round(bytes_[n] / (med * 1e-3) / 1e9, 1),
+                  "GBps_best": round(bytes_[n] / (min(ts) * 1e-3) / 1e9, 1)}
+        print(f"{n:28s} {out[n]}", flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps({"shape": [S, k, m, bs], "results": out}, indent=1))
 
 
 if __name__ == "__main__":

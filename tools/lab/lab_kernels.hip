@@ -459,6 +459,11 @@ const char* lab_dec_name(int v) {
   return (v >= 0 && v < 18) ? names[v] : nullptr;
 }
 
+// Dynamic LDS reserved per ceiling workgroup (residency cap, as the product's
+// xec_set_occupancy); 0 = none.
+static uint32_t g_ceiling_lds = 0;
+void lab_set_ceiling_lds(uint32_t bytes) { g_ceiling_lds = bytes; }
+
 // Bandwidth ceilings on the encode's geometry (k = 16, m = 1): 0 read-only
 // (bytes: S*k*bs), 1 write-only (S*bs), 2 copy of member 0 (2*S*bs).
 int lab_ceiling(int mode, const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, uint64_t m,
@@ -466,9 +471,10 @@ int lab_ceiling(int mode, const void* d, void* p, uint64_t S, uint64_t bs, uint6
   Geo g = geo<64>(S, bs, k, m);
   const uint8_t* dd = static_cast<const uint8_t*>(d);
   uint8_t* pp = static_cast<uint8_t*>(p);
-  if (mode == 0) ceiling<0><<<(uint32_t)g.total, 64, 0, s>>>(dd, pp, g);
-  else if (mode == 1) ceiling<1><<<(uint32_t)g.total, 64, 0, s>>>(dd, pp, g);
-  else ceiling<2><<<(uint32_t)g.total, 64, 0, s>>>(dd, pp, g);
+  const uint32_t lds = g_ceiling_lds;
+  if (mode == 0) ceiling<0><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
+  else if (mode == 1) ceiling<1><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
+  else ceiling<2><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
   return hipGetLastError() == hipSuccess ? 0 : 6;
 }
 
