@@ -202,37 +202,66 @@ def cpu_baseline(k, m, bs, budget_s):
 
 
 def measure_scatter(torch, dist, xec, S_total, S, start, k, m, bs, stream, enc_ms, reps=3):
-    """Config 5's RCCL leg: the whole batch starts on rank 0 and is scattered
-    (point-to-point send/recv over xGMI, xec/dist.py) before the encode.
-    Link-bound, so reported beside -- never as -- the device-resident value."""
+    """Config 5's RCCL legs: the whole batch starts on rank 0,
+    is scattered (point-to-point send/recv over xGMI, xec/dist.py), each rank
+    encodes its slice, and the parity is gathered back to rank 0, where it must
+    equal rank 0's own encode of the whole batch.  Link-bound, so reported
+    beside -- never as -- the device-resident value."""
     from xec import dist as xdist
-    rank = dist.get_rank()
+    rank, world = dist.get_rank(), dist.get_world_size()
+
+    def timed(fn):
+        ts = []
+        for _ in range(reps):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        t = torch.tensor([min(ts)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item()
+
+    def all_true(flag):
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return t.item() == 1.0
+
     full = torch.empty(S_total * k * bs if rank == 0 else 1, dtype=torch.uint8, device="cuda")
     if rank == 0:
         assert xec.fill_splitmix64(full, S_total, k * bs, SEED, stream) == 0
     local = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
-    ts = []
-    for _ in range(reps):
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        xdist.scatter_stripes(full if rank == 0 else None, local, S_total, k * bs)
-        torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
-    t = torch.tensor([min(ts)], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_sc = t.item()
+    t_sc = timed(lambda: xdist.scatter_stripes(full if rank == 0 else None, local, S_total,
+                                               k * bs))
     ref = torch.empty_like(local)
     assert xec.fill_splitmix64(ref, S, k * bs, SEED + start, stream) == 0
-    okt = torch.tensor([1.0 if torch.equal(ref, local) else 0.0], dtype=torch.float64, device="cuda")
-    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    ok = okt.item() == 1.0
-    del full, local, ref
-    moved = (S_total - (S_total // dist.get_world_size())) * k * bs  # bytes leaving rank 0
-    return {"bit_exact": ok, "scatter_ms": round(t_sc * 1e3, 3),
-            "root_egress_GBps": round(moved / t_sc / 1e9, 1),
+    ok_sc = all_true(torch.equal(ref, local))
+    del ref
+    # per-rank encode of the scattered slice, parity gathered back to the root
+    lp = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+    assert xec.encode(local, lp, S, bs, k, m, stream) == 0
+    fullp = torch.empty(S_total * m * bs if rank == 0 else 1, dtype=torch.uint8, device="cuda")
+    t_ga = timed(lambda: xdist.gather_stripes(lp, fullp if rank == 0 else None, S_total, m * bs))
+    ok_ga = True
+    if rank == 0:
+        refp = torch.empty_like(fullp)
+        assert xec.encode(full, refp, S_total, bs, k, m, stream) == 0
+        ok_ga = bool(torch.equal(refp, fullp))
+        del refp
+    ok_ga = all_true(ok_ga)
+    del full, local, lp, fullp
+    a0, b0 = xec.stripe_range(S_total, 0, world)
+    remote = S_total - (b0 - a0)  # stripes that cross a link
+    return {"bit_exact": ok_sc, "scatter_ms": round(t_sc * 1e3, 3),
+            "root_egress_GBps": round(remote * k * bs / t_sc / 1e9, 1),
             "scatter_inclusive_encode_GBps_data": round(
                 S_total * k * bs / (t_sc + enc_ms * 1e-3) / 1e9, 1),
+            "gather_parity_ms": round(t_ga * 1e3, 3),
+            "root_ingress_GBps": round(remote * m * bs / t_ga / 1e9, 1),
+            "scatter_encode_gather_GBps_data": round(
+                S_total * k * bs / (t_sc + enc_ms * 1e-3 + t_ga) / 1e9, 1),
+            "gathered_parity_bit_exact_vs_root_encode": ok_ga,
             "note": "batch starts on rank 0; RCCL send/recv of stripe ranges; link-bound"}
 
 
