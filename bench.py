@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--no-scatter", action="store_true",
                     help="skip the N>1 scatter-inclusive measurement (RCCL send/recv)")
     ap.add_argument("--scatter-timeout", type=float, default=120.0)
+    ap.add_argument("--lost", type=int, default=1,
+                    help="lost data blocks per stripe (1..m, one per parity class); the "
+                         "BASELINE workloads lose one")
     ap.add_argument("--decode-api", default="host", choices=["host", "device"],
                     help="host: xec_decode (reference-shaped: host bitmap scan + H2D copy); "
                          "device: xec_decode_device (bitmap resident, verdict on the device)")
@@ -311,7 +314,7 @@ def main():
         sets.append((d, p, seed_base))
     # single erasure per stripe, (7c) mod k over the GLOBAL stripe index
     import numpy as np
-    bm = erasure_pattern(np, S, k, m, 1, start)
+    bm = erasure_pattern(np, S, k, m, args.lost, start)
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     d_bm = h_bm.to("cuda")
     scratch = [torch.empty_like(d_bm) for _ in range(NSETS)]
@@ -390,6 +393,7 @@ def main():
     elapsed, enc_ms_max, dec_ms_max, bad = t.tolist()
 
     b_enc, b_dec = algorithmic_bytes(S_per, k, m, bs)  # per GPU
+    b_dec *= args.lost
     total_bytes = args.steps * (b_enc + b_dec) * world
     value = total_bytes / elapsed / 1e9
     if rank == 0:
@@ -414,7 +418,7 @@ def main():
               "decode": roofline("xec::decode_kernel", b_dec, dec_ms, traffic_dec)}
         dominant = "decode" if dec_ms >= enc_ms else "encode"
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.lost == 1:  # the CPU leg times one erasure
             cpu = cpu_baseline(k, m, bs, args.cpu_seconds)
         metric = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
         out = {
@@ -432,7 +436,8 @@ def main():
             "data": "synthetic: splitmix64 u64 words, stripe seed 1896+global stripe; generated in HBM",
             "config": {"workload": f"{args.workload}: {desc}", "k": k, "m": m, "block_bytes": bs,
                        "stripes_per_gpu": S_per, "stripes_total": S_total,
-                       "erasure": "data block (7c) mod k lost per stripe",
+                       "erasure": "data block (7c) mod k lost per stripe" if args.lost == 1 else
+                       f"{args.lost} data blocks lost per stripe, one per parity class",
                        "parallelism": f"stripe-partition x{world} (no data-path collective)",
                        "bytes_convention": "algorithmic: enc S(k+m)bs + dec S(k/m+1)bs",
                        "decode_api": "xec_decode_device" if args.decode_api == "device"
