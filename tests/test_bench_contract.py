@@ -52,3 +52,13 @@ def test_bench_device_decode_api():
     stats = out["launch_stats_rank0"]
     assert set(stats) == {"encode", "decode"}
     assert stats["decode"]["min_ms"] <= stats["decode"]["median_ms"] <= stats["decode"]["max_ms"]
+
+
+def test_bench_multi_erasure_line():
+    """--lost 4 at k=16+4: four data blocks lost per stripe (one per class),
+    decode bytes scale with the erasures, verification still bit-exact."""
+    out = run_bench("--workload", "16,4,65536,64", "--lost", "4", "--steps", "3", "--warmup", "1",
+                    "--no-cpu-baseline")
+    assert out["verified"] is True and out["value"] > 0
+    assert out["config"]["erasure"].startswith("4 data blocks lost")
+    assert out["roofline_by_kernel"]["decode"]["algorithmic_bytes_per_launch"] == 4 * 64 * 5 * 65536
