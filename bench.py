@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--lost", type=int, default=1,
                     help="lost data blocks per stripe (1..m, one per parity class); the "
                          "BASELINE workloads lose one")
+    ap.add_argument("--graph", action="store_true",
+                    help="also time the step replayed from one captured hipGraph (needs "
+                         "--decode-api device: the host decode scans and copies on the host)")
     ap.add_argument("--decode-api", default="host", choices=["host", "device"],
                     help="host: xec_decode (reference-shaped: host bitmap scan + H2D copy); "
                          "device: xec_decode_device (bitmap resident, verdict on the device)")
@@ -325,7 +328,7 @@ def main():
     # verified for real after the timed region.
     torch.cuda.synchronize()
 
-    def step(i, ev=None):
+    def step(i, ev=None, stream=stream):
         de, pe, _ = sets[i % NSETS]
         di = (i + NSETS - 1) % NSETS  # the set encoded two kernels ago (module doc)
         dd, pd, _ = sets[di]
@@ -365,6 +368,36 @@ def main():
     dec_list = [e[1].elapsed_time(e[2]) for e in events]
     enc_ms = sum(enc_list) / args.steps
     dec_ms = sum(dec_list) / args.steps
+
+    # ---- optional: the same steps replayed from one captured hipGraph ----------
+    # (xec_decode_device has no host work, so a whole rotation of NSETS steps --
+    # 2*NSETS kernels plus the decode's status memsets and check kernels -- is
+    # one graph; reported beside the headline, never as it)
+    graph = None
+    if args.graph:
+        if args.decode_api != "device":
+            sys.exit("--graph needs --decode-api device")
+        side = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=side):
+            cs = torch.cuda.current_stream()
+            for i in range(NSETS):
+                assert step(i, stream=cs) == 0
+        reps = max(1, args.steps // NSETS)
+        g.replay()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg0 = time.perf_counter()
+        for _ in range(reps):
+            g.replay()
+        torch.cuda.synchronize()
+        tg = time.perf_counter() - tg0
+        assert d_status.tolist() == [0] * NSETS, f"graph decode verdicts {d_status.tolist()}"
+        graph = {"ms_per_step": round(tg / (reps * NSETS) * 1e3, 4), "steps": reps * NSETS,
+                 "note": "one captured rotation of steps replayed; rank-local wall clock"}
+        del g
 
     # ---- correctness of what was timed -------------------------------------
     # parity == XOR of each class's data (encode), then erase -> decode ->
@@ -452,6 +485,7 @@ def main():
             "data_GBps_reference_convention": round(
                 2 * args.steps * S_per * k * bs * world / elapsed / 1e9, 2),
             "verified": bad == 0.0,
+            "graph": graph,
             # per-launch HIP-event statistics on rank 0 (median with stddev)
             "launch_stats_rank0": {
                 n: {"mean_ms": round(statistics.fmean(v), 4),

@@ -62,3 +62,13 @@ def test_bench_multi_erasure_line():
     assert out["verified"] is True and out["value"] > 0
     assert out["config"]["erasure"].startswith("4 data blocks lost")
     assert out["roofline_by_kernel"]["decode"]["algorithmic_bytes_per_launch"] == 4 * 64 * 5 * 65536
+
+
+def test_bench_graph_leg():
+    """--graph replays one captured rotation of encode + device decode steps;
+    the headline line is unchanged and verification still passes."""
+    out = run_bench("--workload", "cfg2", "--stripes", "64", "--steps", "6", "--warmup", "1",
+                    "--no-cpu-baseline", "--decode-api", "device", "--graph")
+    assert out["verified"] is True and out["value"] > 0
+    g = out["graph"]
+    assert g["steps"] == 6 and g["ms_per_step"] > 0
