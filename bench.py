@@ -207,57 +207,79 @@ def cpu_baseline(k, m, bs, budget_s):
     return out
 
 
-def measure_scatter(torch, dist, xec, S_total, S, start, k, m, bs, stream, enc_ms, reps=3):
+class DeviceOps:
+    """What measure_scatter needs from the device: the HIP path by default;
+    tests/test_distributed_cpu.py substitutes CPU stand-ins to run the same
+    scatter / encode / gather logic under gloo."""
+
+    def __init__(self, torch, xec, stream, k, m, bs):
+        self.torch, self.xec, self.stream = torch, xec, stream
+        self.k, self.m, self.bs = k, m, bs
+        self.device = "cuda"
+
+    def fill(self, buf, S, seed_base):
+        assert self.xec.fill_splitmix64(buf, S, self.k * self.bs, seed_base, self.stream) == 0
+
+    def encode(self, d, p, S):
+        assert self.xec.encode(d, p, S, self.bs, self.k, self.m, self.stream) == 0
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+
+def measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms, reps=3):
     """Config 5's RCCL legs: the whole batch starts on rank 0,
     is scattered (point-to-point send/recv over xGMI, xec/dist.py), each rank
     encodes its slice, and the parity is gathered back to rank 0, where it must
     equal rank 0's own encode of the whole batch.  Link-bound, so reported
-    beside -- never as -- the device-resident value."""
+    beside -- never as -- the device-resident value.  `ops` = DeviceOps."""
     from xec import dist as xdist
+    from xec import stripe_range
     rank, world = dist.get_rank(), dist.get_world_size()
+    dev = ops.device
 
     def timed(fn):
         ts = []
         for _ in range(reps):
             dist.barrier()
-            torch.cuda.synchronize()
+            ops.sync()
             t0 = time.perf_counter()
             fn()
-            torch.cuda.synchronize()
+            ops.sync()
             ts.append(time.perf_counter() - t0)
-        t = torch.tensor([min(ts)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([min(ts)], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item()
 
     def all_true(flag):
-        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device="cuda")
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return t.item() == 1.0
 
-    full = torch.empty(S_total * k * bs if rank == 0 else 1, dtype=torch.uint8, device="cuda")
+    full = torch.empty(S_total * k * bs if rank == 0 else 1, dtype=torch.uint8, device=dev)
     if rank == 0:
-        assert xec.fill_splitmix64(full, S_total, k * bs, SEED, stream) == 0
-    local = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+        ops.fill(full, S_total, SEED)
+    local = torch.empty(S * k * bs, dtype=torch.uint8, device=dev)
     t_sc = timed(lambda: xdist.scatter_stripes(full if rank == 0 else None, local, S_total,
                                                k * bs))
     ref = torch.empty_like(local)
-    assert xec.fill_splitmix64(ref, S, k * bs, SEED + start, stream) == 0
+    ops.fill(ref, S, SEED + start)
     ok_sc = all_true(torch.equal(ref, local))
     del ref
     # per-rank encode of the scattered slice, parity gathered back to the root
-    lp = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
-    assert xec.encode(local, lp, S, bs, k, m, stream) == 0
-    fullp = torch.empty(S_total * m * bs if rank == 0 else 1, dtype=torch.uint8, device="cuda")
+    lp = torch.empty(S * m * bs, dtype=torch.uint8, device=dev)
+    ops.encode(local, lp, S)
+    fullp = torch.empty(S_total * m * bs if rank == 0 else 1, dtype=torch.uint8, device=dev)
     t_ga = timed(lambda: xdist.gather_stripes(lp, fullp if rank == 0 else None, S_total, m * bs))
     ok_ga = True
     if rank == 0:
         refp = torch.empty_like(fullp)
-        assert xec.encode(full, refp, S_total, bs, k, m, stream) == 0
+        ops.encode(full, refp, S_total)
         ok_ga = bool(torch.equal(refp, fullp))
         del refp
     ok_ga = all_true(ok_ga)
     del full, local, lp, fullp
-    a0, b0 = xec.stripe_range(S_total, 0, world)
+    a0, b0 = stripe_range(S_total, 0, world)
     remote = S_total - (b0 - a0)  # stripes that cross a link
     return {"bit_exact": ok_sc, "scatter_ms": round(t_sc * 1e3, 3),
             "root_egress_GBps": round(remote * k * bs / t_sc / 1e9, 1),
@@ -512,7 +534,8 @@ def main():
         dog.daemon = True
         dog.start()
         try:
-            sc = measure_scatter(torch, dist, xec, S_total, S, start, k, m, bs, stream, enc_ms)
+            sc = measure_scatter(torch, dist, DeviceOps(torch, xec, stream, k, m, bs), S_total, S,
+                                 start, k, m, bs, enc_ms)
         except Exception as e:  # noqa: BLE001 - report, keep the headline line
             sc = {"error": repr(e)[:200]}
         dog.cancel()

@@ -88,3 +88,66 @@ def test_stripe_range_properties():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         stripe_range(4, 2, 2)
+
+
+class _CpuOps:
+    """CPU stand-ins for bench.DeviceOps: the oracle's fill and encode (test
+    infrastructure), so bench.measure_scatter's scatter -> encode -> gather ->
+    verify logic runs under gloo exactly as it does over RCCL."""
+    device = "cpu"
+
+    def __init__(self, k, m, bs):
+        self.o, self.k, self.m, self.bs = xo.COracle(), k, m, bs
+
+    def fill(self, buf, S, seed_base):
+        if S:
+            d, _ = self.o.batch(S, self.k, self.m, self.bs, seed_base=seed_base)
+            buf.copy_(torch.from_numpy(d.reshape(-1).copy()))
+
+    def encode(self, d, p, S):
+        if S:
+            ld = xo.COracle.aligned(d.numel())
+            ld[:] = d.numpy()
+            lp = xo.COracle.aligned(S * self.m * self.bs)
+            assert self.o.encode_batch(ld, lp, S, self.bs, self.k, self.m, 1) == 0
+            p.copy_(torch.from_numpy(lp.copy()))
+
+    def sync(self):
+        pass
+
+
+def _bench_worker(rank, world, port, S_total, k, m, bs, out_q):
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, b = stripe_range(S_total, rank, world)
+        r = bench.measure_scatter(torch, dist, _CpuOps(k, m, bs), S_total, b - a, a, k, m, bs,
+                                  enc_ms=1.0, reps=1)
+        if rank == 0:
+            out_q.put(r)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,S", [(2, 7), (3, 10), (3, 2)])
+def test_bench_scatter_gather_leg(world, S):
+    """bench.py's N>1 RCCL leg (scatter, per-rank encode, parity gather, checks
+    against the root's own whole-batch encode), run under gloo on the CPU."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, S, 8, 2, 512, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    r = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert r["bit_exact"] is True
+    assert r["gathered_parity_bit_exact_vs_root_encode"] is True
+    assert r["scatter_ms"] > 0 and r["gather_parity_ms"] > 0
