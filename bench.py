@@ -55,7 +55,7 @@ def parse():
                     help=f"one of {sorted(WORKLOADS)}, or a custom shape k,m,bs,S")
     ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline wall budget")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall budget")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (default); gloo only to rehearse N>1 on one GPU")
