@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--decode", action="store_true", help="time the decode diagnostics")
     ap.add_argument("--ceiling", action="store_true", help="time read/write/copy ceilings")
+    ap.add_argument("--wburst", action="store_true",
+                    help="time write-only bursts of 1/4/16 KiB per workgroup, nt vs sc1")
     ap.add_argument("--occ", default="0", help="--ceiling: waves-per-SIMD caps (0 = none), "
                                                "crossed with the product encode's own setting")
     args = ap.parse_args()
@@ -69,6 +71,8 @@ def main():
         return decode_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh)
     if args.ceiling:
         return ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh)
+    if args.wburst:
+        return wburst_lab(args, L, torch, sets, S, k, bs, s, sh)
 
     # correctness of every variant first
     bad = []
@@ -179,6 +183,43 @@ def decode_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):
         b = S * (k + m) * bs if n == "product_encode" else b_dec
         print(f"{n:24s} ms_med {med:.4f}  GBps_med {b / (med * 1e-3) / 1e9:.1f}")
 
+
+
+def wburst_lab(args, L, torch, sets, S, k, bs, s, sh):
+    """Overwrites the data buffers (4 GiB each at the default shape, far past
+    the Infinity Cache); nothing else runs in this mode."""
+    L.lab_wburst.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    L.lab_set_ceiling_lds.argtypes = [ctypes.c_uint32]
+    names = ["1K_nt", "4K_nt", "16K_nt", "1K_sc1", "4K_sc1", "16K_sc1", "4K_by_256thr_nt",
+             "1K_xcdgrp4_nt", "2K_nt", "8K_nt", "1K_xcdgrp4_sc1", "1K_xcdgrp2_nt"]
+    occs = [int(x) for x in args.occ.split(",")]
+    nbytes = S * k * bs
+
+    def run(fn):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.iters)]
+        fn(0)
+        for i in range(args.iters):
+            ev[2 * i].record(s)
+            fn(i + 1)
+            ev[2 * i + 1].record(s)
+        torch.cuda.synchronize()
+        return [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.iters)]
+
+    res = {f"{n}_o{w}": [] for w in occs for n in names}
+    for _ in range(args.rounds):
+        for w in occs:
+            L.lab_set_ceiling_lds(0 if w <= 0 or w >= 8 else ((160 * 1024) // (4 * w)) & ~511)
+            for v, n in enumerate(names):
+                res[f"{n}_o{w}"] += run(lambda i, v=v: L.lab_wburst(
+                    v, sets[i % 2][0].data_ptr(), nbytes, sh))
+    L.lab_set_ceiling_lds(0)
+    out = {}
+    for n, ts in res.items():
+        med = statistics.median(ts)
+        out[n] = {"ms_med": round(med, 4), "GBps_med": round(nbytes / (med * 1e-3) / 1e9, 1)}
+        print(f"{n:16s} {out[n]}", flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps({"bytes": nbytes, "results": out}, indent=1))
 
 
 def ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):

@@ -252,6 +252,45 @@ __global__ __launch_bounds__(64) void ceiling(const uint8_t* data, uint8_t* pari
 }
 
 
+// write-only bursts: each one-wave workgroup stores W KiB contiguous (W
+// 16-byte stores per lane, 1 KiB apart) with cache policy AUX.
+template <int W, int AUX>
+__global__ __launch_bounds__(64) void wburst(uint8_t* out, uint64_t total_bytes) {
+  const uint64_t base = (uint64_t)blockIdx.x * W * 1024;
+  if (base >= total_bytes) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + base, 0, 0x7fffffff, 0x00020000);
+  u32x4 v = {(uint32_t)blockIdx.x, threadIdx.x, 0x9E3779B9u, 0x7F4A7C15u};
+#pragma unroll
+  for (int i = 0; i < W; ++i)
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)(i * 1024 + threadIdx.x * 16), 0, AUX);
+}
+
+// write-only, 1 KiB per one-wave workgroup, but workgroup b writes chunk
+// remap(b): the GRP consecutive chunks of each group go to workgroups b with the
+// same b % 8 (observed: same XCD), so one XCD writes GRP KiB contiguous.
+template <int GRP, int AUX>
+__global__ __launch_bounds__(64) void wburst_xcd(uint8_t* out, uint64_t total_bytes) {
+  const uint64_t b = blockIdx.x;
+  const uint64_t g = b / (8 * GRP), x = b % 8, slot = (b / 8) % GRP;
+  const uint64_t chunk = g * 8 * GRP + x * GRP + slot;
+  const uint64_t base = chunk * 1024;
+  if (base >= total_bytes) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + base, 0, 0x7fffffff, 0x00020000);
+  u32x4 v = {(uint32_t)b, threadIdx.x, 0x9E3779B9u, 0x7F4A7C15u};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)(threadIdx.x * 16), 0, AUX);
+}
+
+// write-only, T-thread workgroups, each lane one 16-byte store: T*16 bytes
+// contiguous per workgroup.
+template <int T>
+__global__ __launch_bounds__(T) void wburst_wg(uint8_t* out, uint64_t total_bytes) {
+  const uint64_t base = (uint64_t)blockIdx.x * T * 16;
+  if (base >= total_bytes) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + base, 0, 0x7fffffff, 0x00020000);
+  u32x4 v = {(uint32_t)blockIdx.x, threadIdx.x, 0x9E3779B9u, 0x7F4A7C15u};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)(threadIdx.x * 16), 0, 2);
+}
+
 // one-wave workgroups that process TPW ADJACENT tiles in sequence (tile
 // b*TPW + i): the store of tile i overlaps the loads of tile i+1.
 template <int NM, int TPW>
@@ -475,6 +514,30 @@ int lab_ceiling(int mode, const void* d, void* p, uint64_t S, uint64_t bs, uint6
   if (mode == 0) ceiling<0><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
   else if (mode == 1) ceiling<1><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
   else ceiling<2><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
+  return hipGetLastError() == hipSuccess ? 0 : 6;
+}
+
+// Write-only burst ceilings over `bytes` of `out`: variant 0..5 =
+// (W, policy) in {1, 4, 16} KiB x {nt, sc1}.
+int lab_wburst(int v, void* out, uint64_t bytes, hipStream_t s) {
+  uint8_t* o = static_cast<uint8_t*>(out);
+  const uint32_t lds = g_ceiling_lds;
+  auto grid = [&](int w) { return (uint32_t)(bytes / (w * 1024ull)); };
+  switch (v) {
+    case 0: wburst<1, 2><<<grid(1), 64, lds, s>>>(o, bytes); break;
+    case 1: wburst<4, 2><<<grid(4), 64, lds, s>>>(o, bytes); break;
+    case 2: wburst<16, 2><<<grid(16), 64, lds, s>>>(o, bytes); break;
+    case 3: wburst<1, 16><<<grid(1), 64, lds, s>>>(o, bytes); break;
+    case 4: wburst<4, 16><<<grid(4), 64, lds, s>>>(o, bytes); break;
+    case 5: wburst<16, 16><<<grid(16), 64, lds, s>>>(o, bytes); break;
+    case 6: wburst_wg<256><<<grid(4), 256, lds, s>>>(o, bytes); break;
+    case 7: wburst_xcd<4, 2><<<grid(1), 64, lds, s>>>(o, bytes); break;
+    case 8: wburst<2, 2><<<grid(2), 64, lds, s>>>(o, bytes); break;
+    case 9: wburst<8, 2><<<grid(8), 64, lds, s>>>(o, bytes); break;
+    case 10: wburst_xcd<4, 16><<<grid(1), 64, lds, s>>>(o, bytes); break;
+    case 11: wburst_xcd<2, 2><<<grid(1), 64, lds, s>>>(o, bytes); break;
+    default: return 1;
+  }
   return hipGetLastError() == hipSuccess ? 0 : 6;
 }
 
