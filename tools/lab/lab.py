@@ -99,13 +99,31 @@ def main():
         torch.cuda.synchronize()
         return [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.iters)]
 
-    res = {names[v]: [] for v in chosen}
-    res["product"] = []
+    # --occ crosses every variant with residency caps: the product via
+    # xec_set_occupancy, lab launches that honour g_ceiling_lds via the same LDS
+    # reservation (only the grouped-tile variants do); 0 = product default / none
+    L.lab_set_ceiling_lds.argtypes = [ctypes.c_uint32]
+    occs = [int(x) for x in args.occ.split(",")]
+
+    def lds(w):
+        return 0 if w <= 0 or w >= 8 else ((160 * 1024) // (4 * w)) & ~511
+
+    def tag(n, w):
+        return n if len(occs) == 1 else f"{n}@o{w}"
+
+    res = {tag(names[v], w): [] for w in occs for v in chosen}
+    res.update({tag("product", w): [] for w in occs})
     for _ in range(args.rounds):
-        res["product"] += run(lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
-        for v in chosen:
-            res[names[v]] += run(lambda i, v=v: L.lab_encode(v, sets[i % 2][0].data_ptr(),
-                                                            sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
+        for w in occs:
+            assert xec.set_occupancy(w) == 0
+            L.lab_set_ceiling_lds(lds(w))
+            res[tag("product", w)] += run(
+                lambda i: xec.encode(sets[i % 2][0], sets[i % 2][1], S, bs, k, m, s))
+            for v in chosen:
+                res[tag(names[v], w)] += run(lambda i, v=v: L.lab_encode(
+                    v, sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(), S, bs, k, m, sh))
+    xec.set_occupancy(0)
+    L.lab_set_ceiling_lds(0)
     out = {}
     for n, ts in res.items():
         med = statistics.median(ts)

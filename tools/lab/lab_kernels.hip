@@ -10,6 +10,10 @@
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Dynamic LDS reserved per workgroup by the launches that honour it (residency
+// cap, as the product's xec_set_occupancy); 0 = none.  Set by lab_set_ceiling_lds.
+static uint32_t g_ceiling_lds = 0;
+
 // cache-policy aux bits for buffer ops on gfx950: sc0 = 1, nt = 2, sc1 = 16
 constexpr int GLOBAL_NT = -1;  // plain global_load/store with __builtin_nontemporal_*
 
@@ -458,7 +462,7 @@ int launch_group(const void* d, void* p, uint64_t S, uint64_t bs, uint64_t k, ui
   if (bs % (UU * 1024)) return 1;
   Geo g = geo<64>(S, bs, k, m);
   static_assert(NM % G == 0, "G must divide the member count");
-  enc_group_impl<NM, G, UU><<<(uint32_t)(S * m * (g.tpb / UU)), 64, 0, s>>>(static_cast<const uint8_t*>(d),
+  enc_group_impl<NM, G, UU><<<(uint32_t)(S * m * (g.tpb / UU)), 64, g_ceiling_lds, s>>>(static_cast<const uint8_t*>(d),
                                                                      static_cast<uint8_t*>(p), g);
   return hipGetLastError() == hipSuccess ? 0 : 6;
 }
@@ -498,9 +502,6 @@ const char* lab_dec_name(int v) {
   return (v >= 0 && v < 18) ? names[v] : nullptr;
 }
 
-// Dynamic LDS reserved per ceiling workgroup (residency cap, as the product's
-// xec_set_occupancy); 0 = none.
-static uint32_t g_ceiling_lds = 0;
 void lab_set_ceiling_lds(uint32_t bytes) { g_ceiling_lds = bytes; }
 
 // Bandwidth ceilings on the encode's geometry (k = 16, m = 1): 0 read-only
