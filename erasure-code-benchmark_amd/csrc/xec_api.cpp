@@ -46,10 +46,11 @@ uint32_t lds_for_occupancy(int waves, int threads) {
 // Resident waves per SIMD that measured fastest for the default shape (one
 // wave per workgroup, one granule per lane), by class member count k/m
 // (tools/sweep.py --occ; profiles/r01i, r01j: two devices, encode and decode,
-// k=4..32).  Each wave has k/m KiB of loads in flight; the best residency keeps
-// about 32 KiB in flight per SIMD (16 KiB at k/m = 4) -- 8 waves of 16 KiB at
-// k/m = 16 crowd HBM with 4x the requests and ran 3 % (encode) to 6 % (decode)
-// slower.  0 = no cap (8 per SIMD).
+// k=4..32).  A wave keeps up to k/m KiB of loads in flight (~11 KiB at k/m =
+// 16, hipcc's rolling window; all 32 at k/m = 32); the best residency keeps
+// roughly 16-32 KiB in flight per SIMD -- 8 waves per SIMD at k/m = 16 queue
+// 4x the requests and ran 3 % (encode) to 6 % (decode) slower.  0 = no cap
+// (8 per SIMD).
 int auto_occupancy(uint64_t nm) {
   switch (nm) {
     case 4: case 8: return 4;
@@ -72,7 +73,8 @@ int decode_auto_occupancy(uint64_t nm, uint64_t lost_data, uint64_t S) {
 }
 
 // Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
-// non-temporal loads and stores (every byte is touched once), one-wave
+// non-temporal loads and parity stores, sc1 rebuilt-block stores (every byte
+// is touched once; xec_kernels.hip kEncodeStoreAux / kDecodeStoreAux), one-wave
 // workgroups with one 1 KiB tile each, one workgroup per tile, residency
 // capped per member count (auto_occupancy).
 xec::LaunchShape launch_shape(size_t bs, int auto_w) {
