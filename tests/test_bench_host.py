@@ -27,3 +27,23 @@ def test_cpu_baseline_shape():
     assert out["unit"] == "GB/s" and out["value"] > 0 and out["cores"] >= 1
     assert out["single_thread"]["value"] > 0
     assert "stripes" in out["sample"]
+
+
+def test_erasure_pattern_is_recoverable_and_exact():
+    """bench.erasure_pattern: `lost` zero data bytes per stripe, each in its own
+    class, parity intact, so every stripe passes is_recoverable
+    (xorec_utils.hpp:160-175) and needs recovery."""
+    import numpy as np
+
+    import xorec_oracle as xo
+    from bench import erasure_pattern
+    for k, m, lost, start in [(16, 1, 1, 0), (16, 4, 4, 5), (32, 8, 8, 3), (8, 2, 2, 17),
+                              (16, 4, 2, 0)]:
+        bm = erasure_pattern(np, 40, k, m, lost, start)
+        assert bm.shape == (40, k + m)
+        assert (bm[:, k:] == 1).all()
+        assert ((bm[:, :k] == 0).sum(axis=1) == lost).all()
+        for row in bm:
+            zeros = np.flatnonzero(row[:k] == 0)
+            assert len(set(zeros % m)) == lost
+            assert xo.np_is_recoverable(k, m, row) and xo.np_require_recovery(k, row)
