@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--decode", action="store_true", help="time the decode diagnostics")
     ap.add_argument("--ceiling", action="store_true", help="time read/write/copy ceilings")
+    ap.add_argument("--dec-sc1", action="store_true",
+                    help="--decode: diagnostics store their result sc1 (the product's policy)")
     ap.add_argument("--wburst", action="store_true",
                     help="time write-only bursts of 1/4/16 KiB per workgroup, nt vs sc1")
     ap.add_argument("--occ", default="0", help="--ceiling: waves-per-SIMD caps (0 = none), "
@@ -140,6 +142,13 @@ def main():
 
 def decode_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):
     import numpy as np
+    # --occ W (first value) caps the diagnostics' residency like the product's;
+    # --dec-sc1 stores their result sc1 like the product's decode
+    w = int(args.occ.split(",")[0])
+    L.lab_set_ceiling_lds.argtypes = [ctypes.c_uint32]
+    L.lab_set_ceiling_lds(0 if w <= 0 or w >= 8 else ((160 * 1024) // (4 * w)) & ~511)
+    L.lab_set_dec_store_aux.argtypes = [ctypes.c_int]
+    L.lab_set_dec_store_aux(16 if args.dec_sc1 else 2)
     L.lab_dec_name.restype = ctypes.c_char_p
     L.lab_dec_name.argtypes = [ctypes.c_int]
     L.lab_decode.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] * 4 + [ctypes.c_void_p]

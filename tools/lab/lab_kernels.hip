@@ -13,12 +13,16 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Dynamic LDS reserved per workgroup by the launches that honour it (residency
 // cap, as the product's xec_set_occupancy); 0 = none.  Set by lab_set_ceiling_lds.
 static uint32_t g_ceiling_lds = 0;
+// Store policy of the decode diagnostics' default modes (2 = nt, as before;
+// 16 = sc1, the product's decode policy).  Set by lab_set_dec_store_aux.
+static int g_dec_store_aux = 2;
 
 // cache-policy aux bits for buffer ops on gfx950: sc0 = 1, nt = 2, sc1 = 16
 constexpr int GLOBAL_NT = -1;  // plain global_load/store with __builtin_nontemporal_*
 
 struct Geo {
   uint64_t S, bs, k, m, tpb, total;
+  int saux;  // decode diagnostics: result store policy (2 = nt, 16 = sc1)
 };
 
 template <int THREADS>
@@ -218,7 +222,10 @@ __global__ __launch_bounds__(64) void dec_wave(uint8_t* data, const uint8_t* par
       dst = data + (c2 * g.k + j) * g.bs + ((7 * c2) % g.k) * stride;
     }
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (uint32_t)off, 0, MODE == 9 ? 0 : (MODE == 10 ? 0x12 : 2));
+    if (MODE == 9) __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (uint32_t)off, 0, 0);
+    else if (MODE == 10) __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (uint32_t)off, 0, 0x12);
+    else if (g.saux == 16) __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (uint32_t)off, 0, 16);
+    else __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (uint32_t)off, 0, 2);
   }
 }
 
@@ -421,7 +428,7 @@ __global__ __launch_bounds__(64) void enc_group_impl(const uint8_t* data, uint8_
 namespace {
 template <int THREADS>
 Geo geo(uint64_t S, uint64_t bs, uint64_t k, uint64_t m) {
-  Geo g{S, bs, k, m, 0, 0};
+  Geo g{S, bs, k, m, 0, 0, 2};
   g.tpb = (bs / 16 + THREADS - 1) / THREADS;
   g.total = S * m * g.tpb;
   return g;
@@ -445,7 +452,8 @@ template <int MODE>
 int launch_dec(void* d, const void* p, const void* lookup, void* out, uint64_t S, uint64_t bs,
                uint64_t k, uint64_t m, uint32_t grid, hipStream_t s) {
   Geo g = geo<64>(S, bs, k, m);
-  dec_wave<16, MODE><<<grid ? grid : (uint32_t)g.total, 64, 0, s>>>(
+  g.saux = g_dec_store_aux;
+  dec_wave<16, MODE><<<grid ? grid : (uint32_t)g.total, 64, g_ceiling_lds, s>>>(
       static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(lookup),
       static_cast<uint8_t*>(out), g);
   return hipGetLastError() == hipSuccess ? 0 : 6;
@@ -503,6 +511,7 @@ const char* lab_dec_name(int v) {
 }
 
 void lab_set_ceiling_lds(uint32_t bytes) { g_ceiling_lds = bytes; }
+void lab_set_dec_store_aux(int aux) { g_dec_store_aux = aux; }
 
 // Bandwidth ceilings on the encode's geometry (k = 16, m = 1): 0 read-only
 // (bytes: S*k*bs), 1 write-only (S*bs), 2 copy of member 0 (2*S*bs).
