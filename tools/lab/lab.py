@@ -268,7 +268,8 @@ def ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):
     def lds(w):  # as csrc/xec_api.cpp lds_for_occupancy for one-wave workgroups
         return 0 if w <= 0 or w >= 8 else ((160 * 1024) // (4 * w)) & ~511
 
-    base = {"read_only_16way": S * k * bs, "write_only": S * bs, "copy": 2 * S * bs}
+    base = {"read_only_16way": S * k * bs, "write_only": S * bs, "copy": 2 * S * bs,
+            "read_only_16way_wg256": S * k * bs, "read_only_16way_wg128": S * k * bs}
     bytes_, res = {}, {}
     for w in occs:
         for n, b in base.items():

@@ -263,6 +263,25 @@ __global__ __launch_bounds__(64) void ceiling(const uint8_t* data, uint8_t* pari
 }
 
 
+// read-only ceiling with T-thread workgroups: each workgroup reads T*16 bytes
+// contiguous of each of the 16 class members (tile of T*16 bytes).
+template <int T>
+__global__ __launch_bounds__(T) void ceiling_read_wg(const uint8_t* data, uint8_t* parity, Geo g) {
+  const uint64_t tpb = g.bs / (T * 16);
+  const uint64_t t = blockIdx.x;
+  if (t >= g.S * tpb) return;
+  const uint64_t c = t / tpb, chunk = t % tpb;
+  const uint8_t* base = data + c * g.k * g.bs + chunk * T * 16 + threadIdx.x * 16;
+  u32x4 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + r * g.bs));
+  u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc ^= v[r];
+  if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u && acc.z == 0xF39CC060u && acc.w == 0x5CEDC834u)
+    parity[0] = 1;
+}
+
 // write-only bursts: each one-wave workgroup stores W KiB contiguous (W
 // 16-byte stores per lane, 1 KiB apart) with cache policy AUX.
 template <int W, int AUX>
@@ -521,6 +540,14 @@ int lab_ceiling(int mode, const void* d, void* p, uint64_t S, uint64_t bs, uint6
   const uint8_t* dd = static_cast<const uint8_t*>(d);
   uint8_t* pp = static_cast<uint8_t*>(p);
   const uint32_t lds = g_ceiling_lds;
+  if (mode == 3) {
+    ceiling_read_wg<256><<<(uint32_t)(S * (bs / 4096)), 256, lds, s>>>(dd, pp, g);
+    return hipGetLastError() == hipSuccess ? 0 : 6;
+  }
+  if (mode == 4) {
+    ceiling_read_wg<128><<<(uint32_t)(S * (bs / 2048)), 128, lds, s>>>(dd, pp, g);
+    return hipGetLastError() == hipSuccess ? 0 : 6;
+  }
   if (mode == 0) ceiling<0><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
   else if (mode == 1) ceiling<1><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
   else ceiling<2><<<(uint32_t)g.total, 64, lds, s>>>(dd, pp, g);
