@@ -5,7 +5,6 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-import xorec_oracle as xo
 
 pytestmark = pytest.mark.gpu
 
