@@ -65,9 +65,10 @@ int auto_occupancy(uint64_t nm) {
 // one erasure per stripe that is the encode table above; with several
 // (tools/sweep.py --lost, profiles/r01p: 16+2, 16+4, 16+8, 32+8, 8+2 at 2..8
 // erasures per stripe) 2 waves per SIMD measured best from 8 loads per tile
-// up (+3 to +15 % over the single-erasure choice), 4 from 4.
+// up (+3 to +15 % over the single-erasure choice), 4 from 4.  Only the member
+// counts those shapes cover (2, 4, 8) take this branch.
 int decode_auto_occupancy(uint64_t nm, uint64_t lost_data, uint64_t S) {
-  if (lost_data <= S) return auto_occupancy(nm);
+  if (lost_data <= S || (nm != 2 && nm != 4 && nm != 8)) return auto_occupancy(nm);
   const uint64_t work = nm * ((lost_data + S - 1) / S);
   return work >= 8 ? 2 : work >= 4 ? 4 : 0;
 }
