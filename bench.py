@@ -15,11 +15,20 @@ the decode of a set and the encode that wrote its parity (and the encode of a
 set and the decode that rewrote its lost blocks) are always two kernels --
 8+ GiB of traffic -- apart.
 
-Multi-GPU: one process per GPU (torchrun); each rank owns a contiguous stripe
-range (xec.partition.stripe_range) -- no collective on the data path; barrier
-+ max-over-ranks timing; value = all ranks' bytes / max time ("weak").
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` starts its own N
+rank processes (launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set per
+child, MASTER_ADDR 127.0.0.1) before anything touches the GPU; under
+torch.distributed.run (WORLD_SIZE already set) it is one of the ranks.  Each
+rank owns a contiguous stripe range (xec.partition.stripe_range) -- no
+collective on the data path; barrier + max-over-ranks timing; value = all
+ranks' bytes / max time ("weak").  RCCL ("nccl") carries the barrier, the
+timing reductions and the config-5 scatter/gather leg.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+`--rehearse-cpu --dist-backend gloo` swaps the device calls for CPU stand-ins
+(tools/cpu_rehearsal.py) to exercise the launcher and the N>1 bookkeeping
+without a GPU; its line is marked as a rehearsal and measures nothing.
 """
 from __future__ import annotations
 
@@ -71,6 +80,15 @@ def parse():
     ap.add_argument("--decode-api", default="host", choices=["host", "device"],
                     help="host: xec_decode (reference-shaped: host bitmap scan + H2D copy); "
                          "device: xec_decode_device (bitmap resident, verdict on the device)")
+    ap.add_argument("--dist-world1", action="store_true",
+                    help="at N=1, still open a one-rank process group (RCCL with nccl) and run "
+                         "the collectives and the scatter/gather leg: exercises the N>1 "
+                         "communication code on a one-GPU box")
+    ap.add_argument("--rehearse-cpu", action="store_true",
+                    help="CPU stand-ins for every device call (tools/cpu_rehearsal.py), gloo "
+                         "only: rehearses the launcher and N>1 bookkeeping; measures nothing")
+    ap.add_argument("--rank-grace", type=float, default=60.0,
+                    help="launcher: seconds to wait for the other ranks after one fails")
     return ap.parse_args()
 
 
@@ -133,77 +151,78 @@ def _cpu_model():
     return model, avx512
 
 
-def cpu_baseline_reference(k, m, bs, budget_s, threads, S):
-    """The reference's own CPU XOR-EC (src/xorec/xorec.cpp, compiled unmodified
-    into oracle/_ref/ref_driver by oracle/Makefile in the build container), run
-    in the CPU plugin's loop (xorec_bm.cpp:27-58: OpenMP over stripes)."""
-    import subprocess
-    drv = ROOT / "oracle" / "_ref" / "ref_driver"
-    if not drv.exists():
-        return None
-    model, avx512 = _cpu_model()
-    version = 3 if avx512 else 2  # XorecVersion AVX512 / AVX2 (xorec_utils.hpp:38-43)
+def _host_threads():
+    """OpenMP threads for the CPU leg: OMP_NUM_THREADS when set (16 on the GPU
+    box, its CPU share), else the CPUs this process may run on."""
     try:
-        p = subprocess.run([str(drv), "bench", str(k), str(m), str(bs), str(S), str(version),
-                            str(threads), str(budget_s)], capture_output=True, text=True,
-                           timeout=budget_s * 4 + 120)
-        r = dict(line.split(" ", 1) for line in p.stdout.strip().splitlines())
-        if p.returncode != 0 or int(r["fail"]) != 0:
-            return None
-        reps, t = int(r["reps"]), float(r["seconds"])
-    except Exception:  # noqa: BLE001 - fall back to the restatement
-        return None
-    b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
-    return {"value": round(reps * (b_enc + b_dec) / t / 1e9, 2), "unit": "GB/s",
-            "cores": threads, "kind": "reference",
-            "sample": f"{reps} x (encode+decode) of {S} stripes k={k}+{m} {bs >> 10} KiB, "
-                      f"reference src/xorec xorec_encode/xorec_decode "
-                      f"(XorecVersion {'AVX512' if version == 3 else 'AVX2'}), OpenMP over "
-                      f"stripes as xorec_bm.cpp:30, {t:.1f} s wall",
-            "cpu_model": model}
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    return max(1, min(t, avail))
 
 
-def cpu_baseline_port(k, m, bs, budget_s, threads, S):
-    """Fallback when oracle/_ref is absent: the oracle's C restatement of the
-    same loop ("port")."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import xorec_oracle as xo  # the CPU baseline leg is the only bench use of oracle/
-
-    o = xo.COracle()
+def cpu_time_port(o, xo, k, m, bs, S, budget_s, threads):
+    """The oracle's C restatement of the reference CPU plugin loop
+    (XorecBenchmark::encode/decode, xorec_bm.cpp:27-58: OpenMP parallel-for over
+    stripes calling xorec_encode / xorec_decode, xorec.cpp:24-111) on one
+    resident host batch, single erasure (7c) mod k per stripe; repeated until
+    `budget_s` of wall time.  Returns (GB/s of algorithmic bytes, reps, seconds)."""
     data, parity = o.batch(S, k, m, bs, threads=threads)
     bm = xo.single_erasure_bitmap(S, k, m)
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
     reps, t_tot = 0, 0.0
-    while t_tot < budget_s and reps < 2000:
+    while (t_tot < budget_s or reps == 0) and reps < 100000:
         t0 = time.perf_counter()
         assert o.encode_batch(data, parity, S, bs, k, m, threads) == 0
         assert o.decode_batch(data, parity, S, bs, k, m, bm, threads) == 0
         t_tot += time.perf_counter() - t0
         reps += 1
-    return {"value": round(reps * (b_enc + b_dec) / t_tot / 1e9, 2), "unit": "GB/s",
-            "cores": threads, "kind": "port",
-            "sample": f"{reps} x (encode+decode) of {S} stripes k={k}+{m} {bs >> 10} KiB "
-                      f"(oracle/xorec_oracle.c, OpenMP over stripes), {t_tot:.1f} s wall",
-            "cpu_model": _cpu_model()[0]}
+    del data, parity
+    return reps * (b_enc + b_dec) / t_tot / 1e9, reps, t_tot
 
 
-def cpu_baseline(k, m, bs, budget_s):
-    """The reference CPU path (xorec_bm.cpp:27-58, OpenMP over stripes) timed on
-    this host on a bounded sample of the same workload: the reference's own code
-    when oracle/_ref was built, else the oracle's C restatement ("port").  Also
-    a short single-thread run of the same code."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
-    S = max(1, (1 << 30) // (k * bs))  # ~1 GiB of data: beyond any host LLC
-    S1 = max(1, (256 << 20) // (k * bs))
-    out = cpu_baseline_reference(k, m, bs, budget_s, threads, S)
-    if out is not None:
-        one = cpu_baseline_reference(k, m, bs, min(2.0, budget_s), 1, S1)
-    else:
-        out = cpu_baseline_port(k, m, bs, budget_s, threads, S)
-        one = cpu_baseline_port(k, m, bs, min(2.0, budget_s), 1, S1)
-    if one is not None:
-        out["single_thread"] = {"value": one["value"], "unit": one["unit"], "sample": one["sample"]}
+CPU_SAMPLE_BYTES = 4 << 30  # ~4 GiB of data per sample: far beyond any host LLC
+
+
+def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, sample_bytes=CPU_SAMPLE_BYTES):
+    """BASELINE.md §2 / SURVEY.md §8(d): the CPU XOR-EC path timed on this host's
+    cores on a bounded sample of the same workload, as the build's restatement
+    (oracle/xorec_oracle.c, "kind": "port"; in-container agreement with the
+    reference's own compiled code: profiles/r02_cpu_port_vs_ref.json), at
+    OMP_NUM_THREADS threads and at 1 thread on the same batch.  Also the other
+    BASELINE shapes (cfg2, cfg3, cfg4) at a third of the budget each, as
+    `by_workload`.  Nothing built from the reference runs here."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import xorec_oracle as xo  # the CPU baseline leg is the only bench use of oracle/
+
+    o = xo.COracle()
+    threads = _host_threads()
+    model = _cpu_model()[0]
+
+    def one(k, m, bs, S_gpu, budget):
+        S = max(1, min(S_gpu, sample_bytes // (k * bs)))
+        v, reps, t = cpu_time_port(o, xo, k, m, bs, S, budget, threads)
+        v1, reps1, t1 = cpu_time_port(o, xo, k, m, bs, S, min(2.0, budget), 1)
+        return {"value": round(v, 2), "unit": "GB/s", "cores": threads, "kind": "port",
+                "sample": f"{reps} x (encode+decode) of {S} stripes k={k}+{m} "
+                          f"{bs >> 10} KiB ({S * k * bs >> 20} MiB data), oracle/xorec_oracle.c "
+                          f"(restates xorec.cpp:24-111), OpenMP over stripes as "
+                          f"xorec_bm.cpp:30, {t:.1f} s wall",
+                "single_thread": {"value": round(v1, 2), "unit": "GB/s",
+                                  "sample": f"{reps1} x the same batch on 1 thread, "
+                                            f"{t1:.1f} s wall"}}
+
+    out = one(k, m, bs, S_gpu, budget_s)
+    out["cpu_model"] = model
+    by = {}
+    for name, (kk, mm, bb, SS, _) in WORKLOADS.items():
+        if name == workload:
+            by[name] = {kx: out[kx] for kx in ("value", "cores", "single_thread", "sample")}
+        else:
+            r = one(kk, mm, bb, SS, budget_s / 3)
+            by[name] = {kx: r[kx] for kx in ("value", "cores", "single_thread", "sample")}
+    out["by_workload"] = by
     return out
 
 
@@ -290,35 +309,111 @@ def measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms, reps=
             "scatter_encode_gather_GBps_data": round(
                 S_total * k * bs / (t_sc + enc_ms * 1e-3 + t_ga) / 1e9, 1),
             "gathered_parity_bit_exact_vs_root_encode": ok_ga,
-            "note": "batch starts on rank 0; RCCL send/recv of stripe ranges; link-bound"}
+            "note": f"batch starts on rank 0; {dist.get_backend()} send/recv of stripe ranges "
+                    "(RCCL over xGMI with nccl); link-bound"}
+
+
+def launch_ranks(n, argv, grace_s):
+    """`bench.py --gpus N` with no launcher around it: start N rank processes of
+    this same script (one per GPU, LOCAL_RANK = device), the environment
+    torch.distributed.run would give them, rendezvous on 127.0.0.1.  Runs
+    before anything imports torch or touches a GPU; children are started, not
+    exec'd.  Rank 0 prints the JSON line; the others print nothing on stdout.
+    Exit status: 0 when every rank exits 0 (or 3, the scatter-leg watchdog,
+    whose error is carried in the line's "scatter" field); else the first
+    failing rank's status, after the others are given `grace_s` and then killed
+    (by PID: only the processes started here)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), XEC_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *argv],
+                                      env=env, cwd=str(ROOT)))
+    rcs = [None] * n
+    t_fail = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if t_fail is None and any(rc not in (None, 0, 3) for rc in rcs):
+            t_fail = time.monotonic()
+        if t_fail is not None and time.monotonic() - t_fail > grace_s:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.kill()
+                    rcs[i] = p.wait()
+        time.sleep(0.05)
+    bad = [(i, rc) for i, rc in enumerate(rcs) if rc not in (0, 3)]
+    if bad:
+        print(f"bench.py launcher: rank exit statuses {rcs}", file=sys.stderr)
+        rc = bad[0][1]
+        return rc if rc > 0 else 1
+    if 3 in rcs:
+        print(f"bench.py launcher: scatter leg watchdog fired on ranks "
+              f"{[i for i, rc in enumerate(rcs) if rc == 3]} (see the line's scatter.error)",
+              file=sys.stderr)
+    return 0
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.rank_grace))
+    run_rank(args)
+
+
+def run_rank(args):
     import torch
     import torch.distributed as dist
-
-    import xec
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-    # one process per GPU; the modulo only matters when rehearsing N>1 on
-    # fewer GPUs (device_count() does not initialise the GPU on this image)
-    dev = local % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(dev)
-    st = xec.init(dev)
-    if st != xec.Status.SUCCESS:
-        sys.exit(f"xec_init({dev}) failed: {st!r}")
+        sys.exit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     backend = args.dist_backend
-    if world > 1:
+    if args.rehearse_cpu:
+        # explicit CPU rehearsal of the launcher / N>1 bookkeeping -- never a fallback
+        if backend != "gloo":
+            sys.exit("--rehearse-cpu needs --dist-backend gloo")
+        if args.graph:
+            sys.exit("--graph needs the GPU")
+        sys.path.insert(0, str(ROOT / "tools"))
+        from cpu_rehearsal import CpuCuda, CpuXec
+        xec, cuda, devname = CpuXec(), CpuCuda(), "cpu"
+    else:
+        import xec
+        cuda, devname = torch.cuda, "cuda"
+    ndev = max(cuda.device_count(), 1)  # does not initialise the GPU on this image
+    if backend == "nccl" and world > ndev:
+        sys.exit(f"--gpus {world} with RCCL needs {world} visible GPUs, found {ndev} "
+                 "(RCCL refuses two ranks on one device; --dist-backend gloo rehearses)")
+    # one process per GPU; the modulo only matters when rehearsing N>1 on
+    # fewer GPUs under gloo
+    dev = local % ndev
+    cuda.set_device(dev)
+    st = xec.init(dev)
+    if st != 0:
+        sys.exit(f"xec_init({dev}) failed: {st!r}")
+    use_dist = world > 1 or args.dist_world1
+    if use_dist:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
+                                    **({} if world > 1 else {
+                                        "init_method": f"tcp://127.0.0.1:{_free_port()}",
+                                        "rank": 0, "world_size": 1}))
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **({} if world > 1 else {
+                "init_method": f"tcp://127.0.0.1:{_free_port()}", "rank": 0, "world_size": 1}))
+        ranks_seen = dist.get_world_size()
+        assert ranks_seen == world, f"process group has {ranks_seen} ranks, expected {world}"
+    coll_dev = devname if backend == "nccl" else "cpu"
 
     k, m, bs, S_per, desc = workload_shape(args.workload)
     if args.stripes:
@@ -326,13 +421,13 @@ def main():
     S_total = S_per * world
     start, stop = xec.stripe_range(S_total, rank, world)
     S = stop - start
-    stream = torch.cuda.current_stream()
+    stream = cuda.current_stream()
 
     # ---- resident inputs: NSETS buffer sets, filled and encoded on the device --
     sets = []
     for s in range(NSETS):
-        d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
-        p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+        d = torch.empty(S * k * bs, dtype=torch.uint8, device=devname)
+        p = torch.empty(S * m * bs, dtype=torch.uint8, device=devname)
         seed_base = SEED + start + s * (1 << 40)
         assert xec.fill_splitmix64(d, S, k * bs, seed_base, stream) == 0
         assert xec.encode(d, p, S, bs, k, m, stream) == 0
@@ -340,15 +435,17 @@ def main():
     # single erasure per stripe, (7c) mod k over the GLOBAL stripe index
     import numpy as np
     bm = erasure_pattern(np, S, k, m, args.lost, start)
-    h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
-    d_bm = h_bm.to("cuda")
+    h_bm = torch.from_numpy(bm.reshape(-1))
+    if devname == "cuda":
+        h_bm = h_bm.pin_memory()
+    d_bm = h_bm.to(devname) if devname == "cuda" else h_bm.clone()
     scratch = [torch.empty_like(d_bm) for _ in range(NSETS)]
-    d_status = torch.full((NSETS,), -1, dtype=torch.int32, device="cuda")
+    d_status = torch.zeros((NSETS,), dtype=torch.int32, device=devname)
     # The lost block's content on entry to decode is irrelevant (include/xec.h),
     # so the timed loop does not re-erase: every decode still reads k/m-1
     # survivors + parity and rewrites the lost block.  Erasure + rebuild is
     # verified for real after the timed region.
-    torch.cuda.synchronize()
+    cuda.synchronize()
 
     def step(i, ev=None, stream=stream):
         de, pe, _ = sets[i % NSETS]
@@ -369,18 +466,18 @@ def main():
 
     for i in range(args.warmup):
         assert step(i) == 0
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    events = [[cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
-    if world > 1:
+    if use_dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    cuda.synchronize()
     t0 = time.perf_counter()
     rc = 0
     for i in range(args.steps):
         rc |= step(args.warmup + i, events[i])
-    torch.cuda.synchronize()
+    cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     assert rc == 0, "xec call failed inside the timed region"
     if args.decode_api == "device":
@@ -408,7 +505,7 @@ def main():
                 assert step(i, stream=cs) == 0
         reps = max(1, args.steps // NSETS)
         g.replay()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
         tg0 = time.perf_counter()
@@ -441,15 +538,28 @@ def main():
             ok &= bool(torch.equal(fresh, d))
         del fresh
 
-    t = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0], dtype=torch.float64,
-                     device="cuda" if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, enc_ms_max, dec_ms_max, bad = t.tolist()
+    # every rank's (elapsed, encode ms, decode ms, failed, stripes); rank 0 reports
+    # the max time over ranks and each rank's own rates
+    mine = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0, float(S)],
+                        dtype=torch.float64, device=coll_dev)
+    if use_dist:
+        rows = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(rows, mine)
+        rows = [r.tolist() for r in rows]
+    else:
+        rows = [mine.tolist()]
+    elapsed = max(r[0] for r in rows)
+    enc_ms_max = max(r[1] for r in rows)
+    dec_ms_max = max(r[2] for r in rows)
+    bad = max(r[3] for r in rows)
+    stripes_done = int(sum(r[4] for r in rows))
 
     b_enc, b_dec = algorithmic_bytes(S_per, k, m, bs)  # per GPU
     b_dec *= args.lost
-    total_bytes = args.steps * (b_enc + b_dec) * world
+    # all ranks' algorithmic bytes (ranges may be ragged only with --stripes
+    # and S_total < world, never at the BASELINE shapes)
+    e_all, d_all = algorithmic_bytes(stripes_done, k, m, bs)
+    total_bytes = args.steps * (e_all + d_all * args.lost)
     value = total_bytes / elapsed / 1e9
     if rank == 0:
         traffic, traffic_src = load_traffic(args.workload)
@@ -473,8 +583,8 @@ def main():
               "decode": roofline("xec::decode_kernel", b_dec, dec_ms, traffic_dec)}
         dominant = "decode" if dec_ms >= enc_ms else "encode"
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and args.lost == 1:  # the CPU leg times one erasure
-            cpu = cpu_baseline(k, m, bs, args.cpu_seconds)
+        if world == 1 and not args.no_cpu_baseline and args.lost == 1 and not args.rehearse_cpu:
+            cpu = cpu_baseline(args.workload, k, m, bs, S_per, args.cpu_seconds)
         metric = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
         out = {
             "metric": metric,
@@ -488,7 +598,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: splitmix64 u64 words, stripe seed 1896+global stripe; generated in HBM",
+            "data": ("CPU REHEARSAL of the launcher and N>1 bookkeeping (tools/cpu_rehearsal.py):"
+                     " not a measurement" if args.rehearse_cpu else
+                     "synthetic: splitmix64 u64 words, stripe seed 1896+global stripe; "
+                     "generated in HBM"),
             "config": {"workload": f"{args.workload}: {desc}", "k": k, "m": m, "block_bytes": bs,
                        "stripes_per_gpu": S_per, "stripes_total": S_total,
                        "erasure": "data block (7c) mod k lost per stripe" if args.lost == 1 else
@@ -505,9 +618,20 @@ def main():
             "encode_GBps_per_gpu": round(b_enc / (enc_ms_max * 1e-3) / 1e9, 1),
             "decode_GBps_per_gpu": round(b_dec / (dec_ms_max * 1e-3) / 1e9, 1),
             "data_GBps_reference_convention": round(
-                2 * args.steps * S_per * k * bs * world / elapsed / 1e9, 2),
+                2 * args.steps * stripes_done * k * bs / elapsed / 1e9, 2),
             "verified": bad == 0.0,
             "graph": graph,
+            "dist": {"backend": dist.get_backend() if use_dist else None,
+                     "ranks_seen": dist.get_world_size() if use_dist else 1,
+                     "launcher": "bench.py" if os.environ.get("XEC_BENCH_SPAWNED") else
+                     ("external" if world > 1 else None)},
+            # each rank's own HIP-event launch rates (weak scaling: same S per rank)
+            "per_rank": [{"rank": i, "stripes": int(r[4]),
+                          "encode_GBps": round(algorithmic_bytes(int(r[4]), k, m, bs)[0]
+                                               / (r[1] * 1e-3) / 1e9, 1) if r[1] else None,
+                          "decode_GBps": round(args.lost * algorithmic_bytes(int(r[4]), k, m, bs)[1]
+                                               / (r[2] * 1e-3) / 1e9, 1) if r[2] else None,
+                          "elapsed_ms": round(r[0] * 1e3, 3)} for i, r in enumerate(rows)],
             # per-launch HIP-event statistics on rank 0 (median with stddev)
             "launch_stats_rank0": {
                 n: {"mean_ms": round(statistics.fmean(v), 4),
@@ -521,21 +645,27 @@ def main():
 
     # Config 5's scatter leg runs after the headline numbers are final, under a
     # watchdog: a stuck link can cost this extra field, never the result line.
-    if world > 1 and backend == "nccl" and not args.no_scatter and not bad:
+    # On expiry every rank exits 3; the bench.py launcher reads 3 as "headline
+    # printed, scatter leg hung" (scatter.error is authoritative), an external
+    # launcher sees the non-zero status.
+    # (gloo cannot carry HIP buffers: with --dist-backend gloo on a GPU the leg is skipped)
+    if use_dist and not args.no_scatter and not bad and (backend == "nccl" or args.rehearse_cpu):
         import threading
 
         def on_timeout():
             if out is not None:
                 out["scatter"] = {"error": f"timed out after {args.scatter_timeout:.0f} s"}
                 print(json.dumps(out), flush=True)
-            os._exit(0)
+            sys.stderr.flush()
+            os._exit(3)
 
         dog = threading.Timer(args.scatter_timeout, on_timeout)
         dog.daemon = True
         dog.start()
         try:
-            sc = measure_scatter(torch, dist, DeviceOps(torch, xec, stream, k, m, bs), S_total, S,
-                                 start, k, m, bs, enc_ms)
+            ops = DeviceOps(torch, xec, stream, k, m, bs)
+            ops.device, ops.sync = coll_dev, cuda.synchronize
+            sc = measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms)
         except Exception as e:  # noqa: BLE001 - report, keep the headline line
             sc = {"error": repr(e)[:200]}
         dog.cancel()
@@ -543,10 +673,17 @@ def main():
             out["scatter"] = sc
     if out is not None:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     if bad:
         sys.exit("verification failed")
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 if __name__ == "__main__":

@@ -54,14 +54,29 @@ int xo_is_recoverable(size_t k, size_t m, const uint8_t* bitmap) {
 }
 
 /* dest ^= src over bytes (bs is a multiple of 256, so every reference
- * variant, xorec.hpp:174-273, covers the whole block and they agree). The
- * clones let one binary pick AVX-512 / AVX2 / SSE2 on whichever host runs it. */
+ * variant, xorec.hpp:174-273, covers the whole block and they agree).  Like
+ * the reference's widest variant it moves 256 B per iteration as four 64-B
+ * vectors (GCC vector extension; the clones let one binary pick AVX-512 /
+ * AVX2 / SSE2 on whichever host runs it), so the CPU baseline times the same
+ * instruction mix (tools/cpu_port_vs_ref.py). */
+typedef uint64_t xo_v64 __attribute__((vector_size(64)));
+
 __attribute__((target_clones("avx512f", "avx2", "default")))
 static void xo_xor_into(uint8_t* __restrict dest, const uint8_t* __restrict src, size_t bytes) {
-  uint64_t* __restrict d = (uint64_t*)__builtin_assume_aligned(dest, 64);
-  const uint64_t* __restrict s = (const uint64_t*)__builtin_assume_aligned(src, 64);
-  size_t n = bytes / 8;
-  for (size_t w = 0; w < n; ++w) d[w] ^= s[w];
+  xo_v64* __restrict d = (xo_v64*)__builtin_assume_aligned(dest, 64);
+  const xo_v64* __restrict s = (const xo_v64*)__builtin_assume_aligned(src, 64);
+  size_t n = bytes / 256;
+  for (size_t w = 0; w < n; ++w, d += 4, s += 4) {
+    const xo_v64 a0 = d[0] ^ s[0], a1 = d[1] ^ s[1], a2 = d[2] ^ s[2], a3 = d[3] ^ s[3];
+    d[0] = a0;
+    d[1] = a1;
+    d[2] = a2;
+    d[3] = a3;
+  }
+  /* bytes % 256 (never on the reference's checked sizes): word by word */
+  uint64_t* dt = (uint64_t*)d;
+  const uint64_t* st = (const uint64_t*)s;
+  for (size_t w = 0; w < (bytes % 256) / 8; ++w) dt[w] ^= st[w];
 }
 
 /* xorec_encode, xorec.cpp:24-59: copy the first m data blocks into parity,

@@ -40,8 +40,12 @@ def test_bench_json_line(workload, stripes):
     assert r["bound"] == "hbm" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     c = out["cpu_baseline"]
-    assert c["kind"] in ("reference", "port") and c["cores"] >= 1 and c["value"] > 0
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
+    assert c["single_thread"]["value"] > 0
+    assert set(c["by_workload"]) == {"cfg2", "cfg3", "cfg4"}
+    assert c["by_workload"][workload]["value"] == c["value"]
     assert out["value"] > 0
+    assert out["dist"]["ranks_seen"] == 1 and len(out["per_rank"]) == 1
 
 
 def test_bench_device_decode_api():
@@ -72,3 +76,25 @@ def test_bench_graph_leg():
     assert out["verified"] is True and out["value"] > 0
     g = out["graph"]
     assert g["steps"] == 6 and g["ms_per_step"] > 0
+
+
+def test_bench_rccl_world1():
+    """The RCCL code path on the one-GPU box: a one-rank nccl process group,
+    barrier / all_gather around the timed region and the scatter/gather leg."""
+    out = run_bench("--workload", "cfg2", "--stripes", "64", "--steps", "3", "--warmup", "1",
+                    "--no-cpu-baseline", "--dist-world1")
+    assert out["verified"] is True
+    assert out["dist"]["backend"] == "nccl" and out["dist"]["ranks_seen"] == 1
+    sc = out["scatter"]
+    assert sc.get("bit_exact") is True, sc
+    assert sc["gathered_parity_bit_exact_vs_root_encode"] is True
+
+
+def test_bench_launcher_two_ranks_one_gpu():
+    """`bench.py --gpus 2` starts both ranks itself; on one GPU they share the
+    device under gloo (RCCL refuses two ranks per device)."""
+    out = run_bench("--gpus", "2", "--dist-backend", "gloo", "--workload", "cfg2", "--stripes",
+                    "32", "--steps", "3", "--warmup", "1")
+    assert out["n_gpus"] == 2 and out["verified"] is True
+    assert out["dist"] == {"backend": "gloo", "ranks_seen": 2, "launcher": "bench.py"}
+    assert out["config"]["stripes_total"] == 64 and len(out["per_rank"]) == 2

@@ -22,11 +22,17 @@ def test_workloads_match_baseline_configs():
 
 
 def test_cpu_baseline_shape():
-    out = bench.cpu_baseline(8, 1, 1 << 16, 0.2)
-    assert out["kind"] in ("reference", "port")
+    """The restatement ("port"), never the reference binary; the bench's own
+    workload plus the other BASELINE shapes; 1-thread figure beside."""
+    out = bench.cpu_baseline("cfg2", 8, 1, 1 << 16, 1024, 0.2, sample_bytes=16 << 20)
+    assert out["kind"] == "port"
     assert out["unit"] == "GB/s" and out["value"] > 0 and out["cores"] >= 1
     assert out["single_thread"]["value"] > 0
-    assert "stripes" in out["sample"]
+    assert "32 stripes" in out["sample"]  # 16 MiB of k=8 x 64 KiB stripes
+    assert set(out["by_workload"]) == {"cfg2", "cfg3", "cfg4"}
+    assert out["by_workload"]["cfg2"]["value"] == out["value"]
+    for w in out["by_workload"].values():
+        assert w["value"] > 0 and w["single_thread"]["value"] > 0
 
 
 def test_erasure_pattern_is_recoverable_and_exact():

@@ -1,0 +1,63 @@
+"""`python bench.py --gpus N` starts its own ranks.
+
+Run as a plain command, the way the driver runs `--gpus 1`, with the explicit
+CPU rehearsal (`--rehearse-cpu --dist-backend gloo`: tools/cpu_rehearsal.py
+stands in for every device call).  What is checked is the launcher and the N>1
+bookkeeping -- rank environment, rendezvous on 127.0.0.1, one JSON line from
+rank 0 only, max-over-ranks timing, per-rank rates, the scatter/gather leg and
+exit-status propagation -- not any number.
+"""
+from __future__ import annotations
+
+import json
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+def _bench(*args, timeout=300):
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True,
+                          text=True, timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_launcher_plain_command(n):
+    p = _bench("--gpus", str(n), "--rehearse-cpu", "--dist-backend", "gloo",
+               "--workload", "8,2,4096,5", "--steps", "3", "--warmup", "1")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n
+    assert out["dist"] == {"backend": "gloo", "ranks_seen": n, "launcher": "bench.py"}
+    assert out["config"]["stripes_total"] == 5 * n
+    assert [r["rank"] for r in out["per_rank"]] == list(range(n))
+    assert all(r["stripes"] == 5 for r in out["per_rank"])
+    assert out["verified"] is True
+    assert out["data"].startswith("CPU REHEARSAL")
+    assert out["cpu_baseline"] is None  # the CPU leg is N=1 only
+    sc = out["scatter"]
+    assert sc["bit_exact"] is True and sc["gathered_parity_bit_exact_vs_root_encode"] is True
+    # max-over-ranks: the reported step time covers every rank's elapsed time
+    assert out["ms_per_step"] * out["steps"] >= max(r["elapsed_ms"] for r in out["per_rank"]) - 1e-3
+
+
+def test_launcher_propagates_rank_failure():
+    # every rank refuses (--rehearse-cpu needs gloo): the launcher must fail too
+    p = _bench("--gpus", "2", "--rehearse-cpu", "--dist-backend", "nccl", "--steps", "1",
+               "--warmup", "0", "--rank-grace", "5", timeout=120)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_world1_process_group_rehearsal():
+    """--dist-world1 opens a one-rank group and runs the collectives + scatter leg."""
+    p = _bench("--rehearse-cpu", "--dist-backend", "gloo", "--dist-world1",
+               "--workload", "4,1,4096,3", "--steps", "2", "--warmup", "1", "--no-cpu-baseline")
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 1 and out["dist"]["ranks_seen"] == 1
+    assert out["scatter"]["bit_exact"] is True
