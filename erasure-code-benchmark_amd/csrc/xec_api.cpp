@@ -26,6 +26,7 @@ std::atomic<int> g_max_grid{0};
 std::atomic<int> g_nt{0};
 std::atomic<int> g_threads{0};
 std::atomic<int> g_occupancy{0};  // xec_set_occupancy: waves per SIMD, 0 = automatic
+std::atomic<int> g_decode_tiling{0};  // xec_set_decode_tiling: 0 auto, 1 stripe, 2 class
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
@@ -67,10 +68,30 @@ int auto_occupancy(uint64_t nm) {
 // erasures per stripe) 2 waves per SIMD measured best from 8 loads per tile
 // up (+3 to +15 % over the single-erasure choice), 4 from 4.  Only the member
 // counts those shapes cover (2, 4, 8) take this branch.
+// The policy reads the batch average, i.e. it assumes the losses are spread
+// evenly over the stripes (as in every measured shape); a batch where a few
+// stripes lose many blocks and most lose none is classed as single-erasure.
 int decode_auto_occupancy(uint64_t nm, uint64_t lost_data, uint64_t S) {
   if (lost_data <= S || (nm != 2 && nm != 4 && nm != 8)) return auto_occupancy(nm);
   const uint64_t work = nm * ((lost_data + S - 1) / S);
   return work >= 8 ? 2 : work >= 4 ? 4 : 0;
+}
+
+// Decode tiling (xec_kernels.hip): stripe tiles run one class reduction per
+// lost data block of their stripe, back to back; class tiles are encode's
+// tiles, one reduction each, but a class without a loss leaves its tiles idle.
+// Measured in one process on both tilings (tools/tiling_ab.py,
+// profiles/r02a/tiling_ab.json; 16+2, 8+2 x 1 MiB, 16+4, 16+8, 32+8 x 64 KiB at
+// 1, m/2 and m losses per stripe): class tiles win once more than one block
+// per stripe AND at least half of the classes are lost (+3 to +9 % with every
+// class lost, +16 % at 16+8 with 4 lost, tie at 32+8 with 4), and lose
+// clearly below that (-6 % at 8+2 with one loss per stripe, 3x slower at
+// 16+8 with one).  With m == 1 the tilings coincide.
+bool use_class_tiles(uint64_t S, uint64_t m, uint64_t lost_data) {
+  const int t = g_decode_tiling.load(std::memory_order_relaxed);
+  if (m <= 1 || t == 1) return false;
+  if (t == 2) return true;
+  return lost_data > S && 2 * lost_data >= S * m;
 }
 
 // Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
@@ -144,9 +165,12 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   if (hipMemcpyAsync(d_bitmap, h_bitmap, S * (k + m), hipMemcpyHostToDevice, stream) !=
       hipSuccess)
     return XEC_DEVICE_ERROR;
-  const xec::LaunchShape ls = launch_shape(bs, decode_auto_occupancy(k / m, lost, S));
+  // class tiles: one reduction per tile, so the encode's residency table
+  const bool cls = use_class_tiles(S, m, lost);
+  const xec::LaunchShape ls =
+      launch_shape(bs, cls ? auto_occupancy(k / m) : decode_auto_occupancy(k / m, lost, S));
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
-  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
+  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, cls, stream) == hipSuccess
              ? XEC_SUCCESS
              : XEC_DEVICE_ERROR;
 }
@@ -157,16 +181,21 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
+  // every argument is checked before any work is queued on the stream
   if (d_status == nullptr || reinterpret_cast<uintptr_t>(d_status) % 4 != 0)
     return XEC_INVALID_ALIGNMENT;
+  if (d_bitmap == nullptr && S != 0) return XEC_INVALID_SIZE;
   if (hipMemsetAsync(d_status, 0, sizeof(int32_t), stream) != hipSuccess) return XEC_DEVICE_ERROR;
   if (S == 0) return XEC_SUCCESS;
-  if (d_bitmap == nullptr) return XEC_INVALID_ALIGNMENT;
+  // No host view of the bitmap: the loss count is unknown, so the tiling is
+  // the stripe tiling with the single-erasure residency table unless
+  // xec_set_decode_tiling(2) says every class lost a block.
+  const bool cls = m > 1 && g_decode_tiling.load(std::memory_order_relaxed) == 2;
   const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   if (xec::launch_check(d_bitmap, g, d_status, stream) != hipSuccess) return XEC_DEVICE_ERROR;
   g.gate = d_status;
-  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, stream) == hipSuccess
+  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, cls, stream) == hipSuccess
              ? XEC_SUCCESS
              : XEC_DEVICE_ERROR;
 }
@@ -227,6 +256,12 @@ xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_
 xec_status xec_set_occupancy(int waves_per_simd) {
   if (waves_per_simd < 0 || waves_per_simd > 8) return XEC_INVALID_SIZE;
   g_occupancy.store(waves_per_simd, std::memory_order_relaxed);
+  return XEC_SUCCESS;
+}
+
+xec_status xec_set_decode_tiling(int tiling) {
+  if (tiling < 0 || tiling > 2) return XEC_INVALID_SIZE;
+  g_decode_tiling.store(tiling, std::memory_order_relaxed);
   return XEC_SUCCESS;
 }
 

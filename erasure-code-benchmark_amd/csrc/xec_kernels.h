@@ -41,16 +41,24 @@ inline Geometry make_geometry(uint64_t S, uint64_t bs, uint64_t k, uint64_t m,
   return g;
 }
 
-inline uint32_t grid_for(uint64_t work_items, uint32_t max_grid) {
-  const uint64_t cap = max_grid ? (uint64_t)max_grid : (uint64_t)0x7fffffffu;
+// Workgroups for `work_items` tiles of a grid-stride kernel: one per tile up
+// to max_grid (0 = no cap of the caller's) and never beyond what HIP accepts,
+// gridDim.x * blockDim.x <= 2^32 - 1; the kernels' grid-stride loops cover the
+// rest.
+inline uint32_t grid_for(uint64_t work_items, uint32_t max_grid, uint32_t threads) {
+  const uint64_t hw = 0xFFFFFFFFull / (threads ? threads : 1);
+  const uint64_t cap = max_grid && max_grid < hw ? (uint64_t)max_grid : hw;
   const uint64_t grid = work_items < cap ? work_items : cap;
   return (uint32_t)(grid ? grid : 1);
 }
 
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
                          const LaunchShape& ls, hipStream_t s);
+// class_tiles: one tile per (stripe, class, chunk) -- for batches where
+// (nearly) every class lost a block; else one per (stripe, chunk).
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
-                         const Geometry& g, const LaunchShape& ls, hipStream_t s);
+                         const Geometry& g, const LaunchShape& ls, bool class_tiles,
+                         hipStream_t s);
 // Device-side recoverability check (xorec_utils.hpp:160-175 over the batch):
 // *d_status |= 4 if some class of some stripe lost two or more blocks.  The
 // caller zeroes *d_status first (stream-ordered).

@@ -231,6 +231,46 @@ __global__ __launch_bounds__(T) void decode_kernel(uint8_t* data, const uint8_t*
 }
 
 // ---------------------------------------------------------------------------
+// decode, class tiles: the tile is encode's (stripe c, class j, column chunk).
+// The workgroup reads its class's k/m data bitmap bytes (scalar dword loads,
+// bytes j, j+m, ... of the stripe's row) and, if one of them is lost -- the
+// host scan guarantees at most one -- rebuilds it with one class reduction,
+// the encode's exact memory shape.  Chosen by the host when (nearly) every
+// class of the batch lost a block (xec_api.cpp decode_tiling): then no tile is
+// idle, and no tile runs several reductions back to back as the stripe tiles
+// above do, whose rebuilt-block store sits in the same vmcnt queue as the
+// next reduction's loads.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t sbyte(uint64_t addr) {
+  const uint32_t w = *(const_u32_as4)(addr & ~3ull);
+  return (w >> (8 * (uint32_t)(addr & 3))) & 0xFFu;
+}
+
+template <int NM, int U, bool NT, int T>
+__global__ __launch_bounds__(T) void decode_class_kernel(uint8_t* data,
+                                                         const uint8_t* __restrict__ parity,
+                                                         const uint8_t* __restrict__ bitmap,
+                                                         Geometry g) {
+  if (g.gate != nullptr && *(const_i32_as4)g.gate != 0) return;
+  const uint32_t nm = NM > 0 ? (uint32_t)NM : (uint32_t)g.nm;
+  const uint64_t stride = g.m * g.bs;
+  for (uint64_t t0 = blockIdx.x; t0 < g.total_tiles; t0 += gridDim.x) {
+    const uint64_t t = g.total_tiles - 1 - t0;  // from the end of the batch, as encode
+    const TileCoord tc = tile_coord(t, g);
+    const uint64_t row = reinterpret_cast<uint64_t>(bitmap + tc.c * (g.k + g.m)) + tc.j;
+    uint32_t lost = nm;
+    for (uint32_t r = 0; r < nm; ++r)
+      if (sbyte(row + (uint64_t)r * g.m) == 0) { lost = r; break; }
+    if (lost == nm) continue;
+    uint8_t* base = data + (tc.c * g.k + tc.j) * g.bs;
+    const uint64_t off = (tc.chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+    xor_members<NM, U, NT, T, kDecodeStoreAux>(base, stride, parity + (tc.c * g.m + tc.j) * g.bs,
+                                               (int)lost, base + (uint64_t)lost * stride, off,
+                                               g.bs, nm);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // check: one thread per (stripe, class); counts the class's lost blocks among
 // its k/m data bytes and its parity byte (is_recoverable, xorec_utils.hpp:160-175).
 // Failure is rare, so the atomic is off the common path.
@@ -300,9 +340,13 @@ hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t g
 
 template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
-                           uint32_t grid, uint32_t lds, hipStream_t s) {
-  decode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<uint8_t*>(d),
-                                                 static_cast<const uint8_t*>(p), bm, g);
+                           bool cls, uint32_t grid, uint32_t lds, hipStream_t s) {
+  if (cls)
+    decode_class_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<uint8_t*>(d),
+                                                         static_cast<const uint8_t*>(p), bm, g);
+  else
+    decode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<uint8_t*>(d),
+                                                   static_cast<const uint8_t*>(p), bm, g);
   return hipGetLastError();
 }
 
@@ -327,9 +371,9 @@ hipError_t enc_nm(const void* d, void* p, const Geometry& g, uint32_t grid, uint
 }
 
 template <int U, bool NT, int T>
-hipError_t dec_nm(void* d, const void* p, const uint8_t* bm, const Geometry& g, uint32_t grid,
-                  uint32_t lds, hipStream_t s) {
-  XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, grid, lds, s)))
+hipError_t dec_nm(void* d, const void* p, const uint8_t* bm, const Geometry& g, bool cls,
+                  uint32_t grid, uint32_t lds, hipStream_t s) {
+  XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, cls, grid, lds, s)))
 }
 
 template <bool NT, int T>
@@ -340,17 +384,17 @@ hipError_t enc_u(const void* d, void* p, const Geometry& g, int unroll, uint32_t
 }
 
 template <bool NT, int T>
-hipError_t dec_u(void* d, const void* p, const uint8_t* bm, const Geometry& g, int unroll,
-                 uint32_t grid, uint32_t lds, hipStream_t s) {
-  return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, grid, lds, s)
-                     : dec_nm<1, NT, T>(d, p, bm, g, grid, lds, s);
+hipError_t dec_u(void* d, const void* p, const uint8_t* bm, const Geometry& g, bool cls,
+                 int unroll, uint32_t grid, uint32_t lds, hipStream_t s) {
+  return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, cls, grid, lds, s)
+                     : dec_nm<1, NT, T>(d, p, bm, g, cls, grid, lds, s);
 }
 
 }  // namespace
 
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
                          const LaunchShape& ls, hipStream_t s) {
-  const uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
+  const uint32_t grid = grid_for(g.total_tiles, ls.max_grid, ls.threads);
   const uint32_t lds = ls.lds_bytes;
   if (ls.threads == 256)
     return ls.nt ? enc_u<true, 256>(d_data, d_parity, g, ls.unroll, grid, lds, s)
@@ -360,21 +404,26 @@ hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
 }
 
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
-                         const Geometry& g_class, const LaunchShape& ls, hipStream_t s) {
-  Geometry g = g_class;  // decode tiles are (stripe, chunk): see decode_kernel
-  g.total_tiles = g.S * g.tiles_per_block;
-  const uint32_t grid = grid_for(g.total_tiles, ls.max_grid);
+                         const Geometry& g_class, const LaunchShape& ls, bool class_tiles,
+                         hipStream_t s) {
+  // stripe tiles (stripe, chunk): decode_kernel; class tiles (stripe, class,
+  // chunk) = encode's tiling: decode_class_kernel.  With m == 1 the two
+  // tilings coincide and the stripe kernel runs.
+  Geometry g = g_class;
+  const bool cls = class_tiles && g.m > 1;
+  if (!cls) g.total_tiles = g.S * g.tiles_per_block;
+  const uint32_t grid = grid_for(g.total_tiles, ls.max_grid, ls.threads);
   const uint32_t lds = ls.lds_bytes;
   if (ls.threads == 256)
-    return ls.nt ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s)
-                 : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s);
-  return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s)
-               : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, ls.unroll, grid, lds, s);
+    return ls.nt ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, cls, ls.unroll, grid, lds, s)
+                 : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, cls, ls.unroll, grid, lds, s);
+  return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, cls, ls.unroll, grid, lds, s)
+               : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, cls, ls.unroll, grid, lds, s);
 }
 
 hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
                         hipStream_t s) {
-  const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192);
+  const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
   check_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status);
   return hipGetLastError();
 }
@@ -382,7 +431,7 @@ hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_s
 hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, const Geometry& g,
                         hipStream_t s) {
   const uint64_t nblocks = g.S * (g.k + g.m);
-  const uint32_t grid = grid_for(nblocks, 65536);
+  const uint32_t grid = grid_for(nblocks, 65536, 256);
   erase_kernel<<<grid, 256, 0, s>>>(static_cast<uint8_t*>(d_data), static_cast<uint8_t*>(d_parity),
                                     d_bitmap, g);
   return hipGetLastError();

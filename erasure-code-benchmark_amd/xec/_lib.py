@@ -25,7 +25,7 @@ EXPORTED = (
     "xec_erase", "xec_fill_splitmix64", "xec_set_launch", "xec_status_string",
     "xec_build_info", "xec_pipeline_create", "xec_pipeline_destroy", "xec_pipeline_encode",
     "xec_pipeline_decode", "xec_write_validation_pattern", "xec_validate_blocks",
-    "xec_decode_device", "xec_set_occupancy",
+    "xec_decode_device", "xec_set_occupancy", "xec_set_decode_tiling",
 )
 
 
@@ -79,6 +79,7 @@ def lib() -> ctypes.CDLL:
         "xec_fill_splitmix64": ([vp, sz, sz, ctypes.c_uint64, vp], st),
         "xec_set_launch": ([ctypes.c_int] * 4, st),
         "xec_set_occupancy": ([ctypes.c_int], st),
+        "xec_set_decode_tiling": ([ctypes.c_int], st),
         "xec_status_string": ([st], ctypes.c_char_p),
         "xec_build_info": ([], ctypes.c_char_p),
         "xec_pipeline_create": ([ctypes.POINTER(vp), sz, sz, sz, sz, ctypes.c_int], st),

@@ -104,6 +104,12 @@ def set_occupancy(waves_per_simd: int = 0) -> Status:
     return Status(lib().xec_set_occupancy(waves_per_simd))
 
 
+def set_decode_tiling(tiling: int = 0) -> Status:
+    """xec_set_decode_tiling; 0 = automatic (default), 1 = stripe tiles, 2 = class tiles
+    (m > 1 only; identical results)."""
+    return Status(lib().xec_set_decode_tiling(tiling))
+
+
 def status_string(st: int) -> str:
     return lib().xec_status_string(int(st)).decode()
 

@@ -89,8 +89,12 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
  * *d_status != 0 (all-or-nothing, like xec_decode) and otherwise rebuilds
  * every lost data block exactly as xec_decode does.  The return value covers
  * only what the host can check (argument errors as xec_decode, d_status
- * null or not 4-B aligned -> XEC_INVALID_ALIGNMENT, launch failure); the batch
- * verdict is *d_status (device int32), valid once the stream reaches it. */
+ * null or not 4-B aligned -> XEC_INVALID_ALIGNMENT, d_bitmap null with S > 0
+ * -> XEC_INVALID_SIZE, launch failure); nothing is queued on `stream` when an
+ * argument is rejected.  The batch verdict is *d_status (device int32), valid
+ * once the stream reaches it.  Tiling: stripe tiles with the single-erasure
+ * residency table (no host view of the loss count), unless
+ * xec_set_decode_tiling(2). */
 xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                              size_t m, const uint8_t* d_bitmap, int32_t* d_status,
                              hipStream_t stream);
@@ -149,6 +153,18 @@ xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_
  * users off those CUs while a launch runs.  Returns XEC_INVALID_SIZE outside
  * 0..8. */
 xec_status xec_set_occupancy(int waves_per_simd);
+
+/* Tuning / diagnostics (no reference counterpart): how decode tiles the
+ * batch when m > 1.  0 = automatic (default): xec_decode counts the lost data
+ * blocks in its host scan and uses class tiles -- one tile per (stripe,
+ * class, 1 KiB column chunk), one class reduction each, encode's tiling --
+ * when the batch lost more than one data block per stripe on average and at
+ * least half of its S*m classes lost one, else stripe
+ * tiles -- one per (stripe, chunk), rebuilding the stripe's lost blocks one
+ * after another; xec_decode_device (no host scan) uses stripe tiles.
+ * 1 = always stripe tiles, 2 = always class tiles.  Results are identical;
+ * only the speed differs.  XEC_INVALID_SIZE outside 0..2. */
+xec_status xec_set_decode_tiling(int tiling);
 
 /* ---- host-in / host-out pipeline --------------------
  * The MI355X analogue of the reference's GPU-memory / unified-memory variants

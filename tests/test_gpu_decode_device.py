@@ -158,8 +158,13 @@ def test_device_argument_errors_and_empty_batch(gpu):
     assert gpu.decode_device(d, p, 1, 100, 4, 1, bm, st) == S_.INVALID_SIZE
     assert gpu.decode_device(d.data_ptr() + 16, p, 1, 4096, 4, 1, bm, st) == S_.INVALID_ALIGNMENT
     assert gpu.decode_device(d, p, 1, 4096, 6, 4, bm, st) == S_.INVALID_COUNTS
+    assert gpu.decode_device(d, p, 1, 4096, 4, 1, 0, st) == S_.INVALID_SIZE  # null bitmap
     torch.cuda.synchronize()
     assert st.tolist() == [9, 9, 9, 9], "argument errors must enqueue nothing"
+    assert gpu.decode_device(d, p, 0, 4096, 4, 1, 0, st[1:]) == S_.SUCCESS  # S=0: bitmap unused
+    torch.cuda.synchronize()
+    assert st.tolist() == [9, 0, 9, 9]
+    st[1] = 9
     assert gpu.decode_device(d, p, 0, 4096, 4, 1, bm, st) == S_.SUCCESS
     torch.cuda.synchronize()
     assert st.tolist() == [0, 9, 9, 9]

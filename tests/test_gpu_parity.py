@@ -225,3 +225,81 @@ def test_encode_is_linear(gpu):
         assert gpu.encode(x, px, S, bs, k, m, a.stream) == 0
     torch.cuda.synchronize()
     assert torch.equal(torch.bitwise_xor(a.p, bb.p), pab)
+
+
+@pytest.mark.parametrize("tiling", [0, 1, 2])
+@pytest.mark.parametrize("S,k,m,bs,pattern", [
+    (64, 16, 2, 65536, "all"),      # every class lost a data block: class tiles (auto)
+    (48, 16, 8, 8192, "all"),
+    (40, 32, 8, 4352, "all"),       # ragged tail tile
+    (33, 8, 2, 2048, "all"),
+    (50, 16, 4, 4096, "half"),      # half the classes: class tiles with idle tiles (auto)
+    (50, 16, 4, 4096, "one"),       # one per stripe: stripe tiles (auto)
+    (30, 12, 4, 1024, "parity"),    # lost parity + lost data in other classes
+    (21, 24, 8, 1024, "select"),    # reference select_lost_blocks, 1..m per stripe
+    (9, 10, 5, 768, "all"),         # generic member count (k/m = 2, m = 5)
+    (7, 15, 5, 512, "all"),         # generic member count 3
+])
+def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
+    """xec_set_decode_tiling: stripe tiles, class tiles and the automatic choice
+    rebuild the same bytes, whatever fraction of the classes lost a block."""
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    bm = np.ones((S, k + m), np.uint8)
+    rng = np.random.default_rng(S * 1000 + k)
+    for c in range(S):
+        if pattern == "all":
+            for j in range(m):
+                bm[c, j + m * int(rng.integers(k // m))] = 0
+        elif pattern == "half":
+            for j in range(0, m, 2):
+                bm[c, j + m * int(rng.integers(k // m))] = 0
+        elif pattern == "one":
+            bm[c, int(rng.integers(k))] = 0
+        elif pattern == "parity":
+            lost_par = int(rng.integers(m))
+            bm[c, k + lost_par] = 0
+            for j in range(m):
+                if j != lost_par:
+                    bm[c, j + m * int(rng.integers(k // m))] = 0
+        else:
+            oracle.select_lost_blocks(k, m, 1 + c % m, bm[c], 300 + c)
+    assert gpu.set_decode_tiling(tiling) == gpu.Status.SUCCESS
+    try:
+        erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+    finally:
+        gpu.set_decode_tiling(0)
+
+
+@pytest.mark.parametrize("tiling", [1, 2])
+def test_golden_decode_fixtures_each_tiling(gpu, oracle, known_answers, tiling):
+    assert gpu.set_decode_tiling(tiling) == gpu.Status.SUCCESS
+    try:
+        test_golden_decode_fixtures(gpu, oracle, known_answers)
+    finally:
+        gpu.set_decode_tiling(0)
+
+
+def test_decode_tiling_argument_range(gpu):
+    assert gpu.set_decode_tiling(3) == gpu.Status.INVALID_SIZE
+    assert gpu.set_decode_tiling(-1) == gpu.Status.INVALID_SIZE
+    assert gpu.set_decode_tiling(0) == gpu.Status.SUCCESS
+
+
+def test_grid_beyond_hip_launch_limit(gpu):
+    """More tiles than HIP accepts workgroups in one launch (gridDim.x * 64 >
+    2^32 - 1): the default grid is capped and the kernels grid-stride over the
+    rest.  k == m == 1 makes parity a copy of data, checked on the device."""
+    torch = _torch()
+    S, bs = (1 << 26) + 5, 1024  # 2^26 + 5 one-KiB tiles: 64 GiB data + 64 GiB parity
+    free, _ = torch.cuda.mem_get_info()
+    if free < 2 * S * bs + (8 << 30):
+        pytest.skip(f"needs {2 * S * bs >> 30} GiB of free HBM")
+    d = torch.empty(S * bs, dtype=torch.uint8, device="cuda")
+    assert gpu.fill_splitmix64(d, S, bs, 5, torch.cuda.current_stream()) == 0
+    p = torch.zeros_like(d)
+    assert gpu.encode(d, p, S, bs, 1, 1, torch.cuda.current_stream()) == gpu.Status.SUCCESS
+    torch.cuda.synchronize()
+    assert torch.equal(d[-(1 << 20):], p[-(1 << 20):])
+    assert torch.equal(d, p)
+    del d, p
+    torch.cuda.empty_cache()

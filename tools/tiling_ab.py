@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""In-process A/B of the decode tilings (xec_set_decode_tiling) on one MI355X.
+
+For each shape and each number of lost data blocks per stripe (one per class,
+bench.erasure_pattern), times xec_decode with stripe tiles (1), class tiles (2)
+and the automatic choice (0) in interleaved rounds on the same buffers (three
+rotating buffer sets, HIP events on the launching stream), and checks every
+variant rebuilt the erased blocks bit-exactly (against a fresh device fill).
+Also times encode on the same buffers as the reference point.  Rates are
+algorithmic GB/s: decode S*lost*(k/m+1)*bs, encode S*(k+m)*bs per launch.
+
+    python tools/tiling_ab.py [--shapes 16,2,1048576,256:16,8,65536,16384] [--out f.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
+
+from bench import algorithmic_bytes, erasure_pattern  # noqa: E402
+
+DEFAULT_SHAPES = "16,2,1048576,256:16,8,65536,16384:32,8,65536,8192:16,4,65536,16384:8,2,1048576,256"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default=DEFAULT_SHAPES)
+    ap.add_argument("--lost", default="", help="comma list; default 1, m/2, m (distinct)")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import xec
+
+    torch.cuda.set_device(0)
+    assert xec.init(0) == 0
+    stream = torch.cuda.current_stream()
+    results = []
+    for shape in args.shapes.split(":"):
+        k, m, bs, S = (int(x) for x in shape.split(","))
+        losts = ([int(x) for x in args.lost.split(",")] if args.lost
+                 else sorted({1, max(1, m // 2), m}))
+        sets = []
+        for s in range(3):
+            d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+            p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+            assert xec.fill_splitmix64(d, S, k * bs, 1000 + s * 7919, stream) == 0
+            assert xec.encode(d, p, S, bs, k, m, stream) == 0
+            sets.append((d, p))
+        b_enc, b_dec1 = algorithmic_bytes(S, k, m, bs)
+        for lost in losts:
+            if lost > m:
+                continue
+            bm = erasure_pattern(np, S, k, m, lost)
+            h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
+            d_bm = h_bm.to("cuda")
+            scratch = [torch.empty_like(d_bm) for _ in range(3)]
+            variants = {"stripe": 1, "class": 2, "auto": 0} if m > 1 else {"stripe": 1}
+            times = {v: [] for v in variants}
+            times["encode"] = []
+            it = 0
+            for _ in range(args.rounds):
+                for v, t in list(variants.items()) + [("encode", None)]:
+                    if t is not None:
+                        assert xec.set_decode_tiling(t) == 0
+                    evs = [(torch.cuda.Event(enable_timing=True),
+                            torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
+                    for i in range(args.iters):
+                        d, p = sets[it % 3]
+                        it += 1
+                        evs[i][0].record(stream)
+                        if v == "encode":
+                            assert xec.encode(d, p, S, bs, k, m, stream) == 0
+                        else:
+                            assert xec.decode(d, p, S, bs, k, m, h_bm, scratch[it % 3], stream) == 0
+                        evs[i][1].record(stream)
+                    torch.cuda.synchronize()
+                    times[v] += [a.elapsed_time(b) for a, b in evs]
+            # correctness of each variant: erase -> decode -> == fresh fill
+            fresh = torch.empty_like(sets[0][0])
+            ok = {}
+            for v, t in variants.items():
+                assert xec.set_decode_tiling(t) == 0
+                d, p = sets[0]
+                assert xec.erase(d, p, S, bs, k, m, d_bm, stream) == 0
+                assert xec.decode(d, p, S, bs, k, m, h_bm, scratch[0], stream) == 0
+                assert xec.fill_splitmix64(fresh, S, k * bs, 1000, stream) == 0
+                ok[v] = bool(torch.equal(fresh, d))
+            assert xec.set_decode_tiling(0) == 0
+            del fresh
+            b_dec = b_dec1 * lost
+            row = {"k": k, "m": m, "bs": bs, "S": S, "lost_per_stripe": lost,
+                   "class_fraction": lost / m, "bit_exact": ok}
+            for v, ts in times.items():
+                med = statistics.median(ts)
+                b = b_enc if v == "encode" else b_dec
+                row[v] = {"median_ms": round(med, 4), "GBps": round(b / med / 1e6, 1),
+                          "frac_8TBps": round(b / med / 1e6 / 8000, 4)}
+            print(json.dumps(row), flush=True)
+            results.append(row)
+        del sets
+        torch.cuda.empty_cache()
+    if args.out:
+        Path(args.out).write_text(json.dumps(results, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
