@@ -10,6 +10,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <tuple>
+#include <vector>
 
 namespace xec {
 
@@ -35,6 +36,17 @@ struct BenchmarkConfig {
                                 // (hipSetDeviceFlags; CUDA's default "auto" spins when
                                 // contexts < cores, which is what the reference ran under)
 };
+
+// The reference's sweep vectors (src/benchmark/bm_config.cpp:3-23,
+// bm_config.hpp:51) from which get_gpu_configs (benchmark_suite.cpp:252-277)
+// forms the GPU cross product.
+constexpr size_t kMessageSize = 8u << 20;  // MESSAGE_SIZE = 8 MiB
+inline const std::vector<size_t> kVarBlockSizes = {1u << 10, 2u << 10, 4u << 10, 8u << 10};
+inline const std::vector<ECTuple> kVarEcParams = {
+    {4 + 8, 8}, {4 + 16, 16}, {8 + 16, 16}, {4 + 32, 32}, {8 + 32, 32}};
+inline const std::vector<size_t> kVarNumLostBlocks = {0, 1, 2, 4, 8};
+inline const std::vector<size_t> kVarNumGpuBlocks = {256};
+inline const std::vector<size_t> kVarNumThreadsPerBlock = {512};
 
 inline size_t data_blocks(const BenchmarkConfig& c) { return std::get<1>(c.ec_params); }
 inline size_t parity_blocks(const BenchmarkConfig& c) {

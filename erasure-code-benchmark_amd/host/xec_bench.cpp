@@ -1,25 +1,47 @@
-// xec_bench.cpp -- command-line harness: the reference's "xorec-gpu" benchmark
-// (BM_XOREC_GPU_CMP, src/benchmark/runners.cpp:43-45) re-registered as
-// "xorec-hip", one CSV row per configuration in the reference's schema.
+// xec_bench.cpp -- command-line harness with the reference's CLI contract
+// (src/utils/benchmark_suite.cpp:102-212) for the HIP XOR-EC plugin,
+// registered as GPU algorithm "xorec-hip" beside the reference's "xorec-gpu"
+// (benchmark_suite.cpp:56-62; runners.cpp:43-45).
 //
-//   xec_bench [-s message_bytes] [-b block_bytes] [-k data] [-m parity]
-//             [-l lost_per_stripe] [-i iterations] [-w warmup] [-t cpu_threads]
-//             [-d device] [-r seed] [-o out.csv] [--no-header] [-f sweep_file]
-//             [-y sync_mode: 0 default, 1 spin, 2 yield, 3 blocking]
-//             [-V: validation payload on the host + copies, as the reference]
-// -f runs every line "message_bytes block_bytes k m lost" of sweep_file in
-// this process (one CSV row each), like the reference's config cross-product
-// (benchmark_suite.cpp:220-318).
-// Sizes accept K/M/G suffixes (binary).  Defaults: BASELINE.json configs[2]
-// (k=16+1, 1 MiB blocks, 256 stripes = 4 GiB message), 1 lost block, 10
-// iterations, 0 warm-up (the reference's defaults, benchmark_suite.cpp:30-31).
+//   xec_bench -g xorec-hip [-f out.csv] [-a] [-i iters] [-w warmup] [-s simd,...] [-h]
+//
+//   -f, --file        output CSV (must contain ".csv"; default results.csv), written
+//                     at the given path (the reference prefixes ../results/raw/)
+//   -a, --append      append rows without a header (default: overwrite + header,
+//                     csv_reporter.cpp:11-19)
+//   -i, --iterations  timed iterations per config (> 0, default 10)
+//   -w, --warmup      warm-up iterations per config (>= 0, default 0)
+//   -g, --gpu         GPU algorithms, comma separated: xorec-hip
+//   -c, --cpu         CPU algorithms are outside this build (error)
+//   -s, --simd        CPU XOR-EC SIMD versions (scalar, sse2, avx2, avx512): validated
+//                     like the reference; they select CPU variants only, so no effect here
+// With -g and no config options, the configs are the reference's GPU cross
+// product (get_gpu_configs, benchmark_suite.cpp:252-277, over the vectors of
+// bm_config.cpp:3-23): 8 MiB messages x block sizes x EC params x lost blocks
+// (<= m) x 256 GPU blocks x 512 threads, one 20-column CSV row each, in the
+// reference's order.
+//
+// Extensions (long options only):
+//   --message B --block B --data K --parity M --lost L   one config instead of the sweep
+//                                    (sizes accept K/M/G suffixes, binary)
+//   --sweep FILE     configs from FILE, one "message block k m lost" per line
+//   --threads N      host threads for host-side validation (default: all)
+//   --device D       HIP device (default 0)
+//   --seed S         seed of payloads and erasure draws (the reference uses the clock)
+//   --sync MODE      hipSetDeviceFlags: 0 default, 1 spin, 2 yield, 3 blocking
+//   --host-validation  payload written/checked on the host + copies, as the reference
+//   --stdout         CSV to stdout instead of -f
+#include <getopt.h>
 #include <omp.h>
 
+#include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -27,6 +49,8 @@
 #include "xorec_hip_bm.hpp"
 
 namespace {
+
+const char* kName = "XOR-EC (HIP gfx950)";
 
 size_t parse_size(const char* s) {
   char* end = nullptr;
@@ -40,93 +64,219 @@ size_t parse_size(const char* s) {
   return static_cast<size_t>(v);
 }
 
+// get_arg_vector (benchmark_suite.cpp:75-83): comma split, lower case
+std::vector<std::string> arg_vector(const char* s) {
+  std::vector<std::string> out;
+  std::stringstream ss(s);
+  std::string tok;
+  while (std::getline(ss, tok, ',')) {
+    std::transform(tok.begin(), tok.end(), tok.begin(),
+                   [](unsigned char c) { return static_cast<char>(std::tolower(c)); });
+    out.push_back(tok);
+  }
+  return out;
+}
+
 void usage() {
-  std::fprintf(stderr,
-               "usage: xec_bench [-s message_bytes] [-b block_bytes] [-k data] [-m parity]\n"
-               "                 [-l lost] [-i iters] [-w warmup] [-t threads] [-d device]\n"
-               "                 [-r seed] [-o out.csv] [--no-header] [-f sweep_file]\n"
-               "                 [-y sync_mode] [-V]\n");
+  std::printf(
+      "usage: xec_bench -g xorec-hip [-f out.csv] [-a] [-i iters] [-w warmup] [-s simd,...]\n"
+      "  -f, --file FILE        output CSV (must contain .csv; default results.csv)\n"
+      "  -a, --append           append rows, no header (default: overwrite + header)\n"
+      "  -i, --iterations N     timed iterations per config (default 10)\n"
+      "  -w, --warmup N         warm-up iterations per config (default 0)\n"
+      "  -g, --gpu LIST         GPU algorithms: xorec-hip\n"
+      "  -c, --cpu LIST         CPU algorithms: none in this build\n"
+      "  -s, --simd LIST        scalar,sse2,avx2,avx512 (CPU variants only; no effect)\n"
+      "  -h, --help\n"
+      "extensions: --message B --block B --data K --parity M --lost L | --sweep FILE\n"
+      "            --threads N --device D --seed S --sync MODE --host-validation --stdout\n"
+      "without config options -g runs the reference's GPU sweep (get_gpu_configs)\n");
+}
+
+[[noreturn]] void fail(const std::string& msg) {
+  std::cerr << "Error: " << msg << '\n';
+  std::exit(EXIT_FAILURE);
+}
+
+// get_gpu_configs (benchmark_suite.cpp:252-277), same loop order
+std::vector<xec::BenchmarkConfig> gpu_sweep(const xec::BenchmarkConfig& base) {
+  std::vector<xec::BenchmarkConfig> out;
+  for (size_t bs : xec::kVarBlockSizes)
+    for (const auto& ec : xec::kVarEcParams) {
+      const size_t m = std::get<0>(ec) - std::get<1>(ec);
+      for (size_t lost : xec::kVarNumLostBlocks) {
+        if (lost > m) continue;
+        for (size_t gb : xec::kVarNumGpuBlocks)
+          for (size_t tpb : xec::kVarNumThreadsPerBlock) {
+            xec::BenchmarkConfig c = base;
+            c.message_size = xec::kMessageSize;
+            c.block_size = bs;
+            c.ec_params = ec;
+            c.num_lost_blocks = lost;
+            c.num_cpu_threads = 0;  // as the reference's GPU configs
+            c.gpu_computation = true;
+            c.num_gpu_blocks = gb;
+            c.threads_per_gpu_block = tpb;
+            out.push_back(c);
+          }
+      }
+    }
+  return out;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
-  xec::BenchmarkConfig cfg;
+  enum { kMessage = 1000, kBlock, kData, kParity, kLost, kSweep, kThreads, kDevice, kSeed, kSync,
+         kHostVal, kStdout };
+  const option long_options[] = {
+      {"help", no_argument, nullptr, 'h'},
+      {"file", required_argument, nullptr, 'f'},
+      {"append", no_argument, nullptr, 'a'},
+      {"iterations", required_argument, nullptr, 'i'},
+      {"warmup", required_argument, nullptr, 'w'},
+      {"cpu", required_argument, nullptr, 'c'},
+      {"gpu", required_argument, nullptr, 'g'},
+      {"simd", required_argument, nullptr, 's'},
+      {"message", required_argument, nullptr, kMessage},
+      {"block", required_argument, nullptr, kBlock},
+      {"data", required_argument, nullptr, kData},
+      {"parity", required_argument, nullptr, kParity},
+      {"lost", required_argument, nullptr, kLost},
+      {"sweep", required_argument, nullptr, kSweep},
+      {"threads", required_argument, nullptr, kThreads},
+      {"device", required_argument, nullptr, kDevice},
+      {"seed", required_argument, nullptr, kSeed},
+      {"sync", required_argument, nullptr, kSync},
+      {"host-validation", no_argument, nullptr, kHostVal},
+      {"stdout", no_argument, nullptr, kStdout},
+      {nullptr, 0, nullptr, 0}};
+
+  xec::BenchmarkConfig base;
+  base.num_iterations = 10;        // NUM_ITERATIONS (benchmark_suite.cpp:30)
+  base.num_warmup_iterations = 0;  // NUM_WARMUP_ITERATIONS (:31)
+  base.gpu_computation = true;
+  base.num_gpu_blocks = xec::kVarNumGpuBlocks[0];
+  base.threads_per_gpu_block = xec::kVarNumThreadsPerBlock[0];
+  base.num_cpu_threads = static_cast<size_t>(omp_get_max_threads());
+  // single-config defaults: BASELINE.json configs[2] (k=16+1, 1 MiB blocks,
+  // 256 stripes = 4 GiB message, 1 lost block per stripe)
+  xec::BenchmarkConfig single = base;
   size_t k = 16, m = 1;
-  cfg.block_size = 1 << 20;
-  cfg.message_size = 256ull * 16 * (1 << 20);
-  cfg.num_lost_blocks = 1;
-  cfg.num_cpu_threads = static_cast<size_t>(omp_get_max_threads());
-  std::string out, sweep;
-  bool header = true;
-  for (int i = 1; i < argc; ++i) {
-    std::string a = argv[i];
-    auto val = [&]() -> const char* {
-      if (i + 1 >= argc) { usage(); std::exit(2); }
-      return argv[++i];
-    };
-    if (a == "-s") cfg.message_size = parse_size(val());
-    else if (a == "-b") cfg.block_size = parse_size(val());
-    else if (a == "-k") k = parse_size(val());
-    else if (a == "-m") m = parse_size(val());
-    else if (a == "-l") cfg.num_lost_blocks = parse_size(val());
-    else if (a == "-i") cfg.num_iterations = std::atoi(val());
-    else if (a == "-w") cfg.num_warmup_iterations = std::atoi(val());
-    else if (a == "-t") cfg.num_cpu_threads = parse_size(val());
-    else if (a == "-d") cfg.device_id = std::atoi(val());
-    else if (a == "-r") cfg.seed = parse_size(val());
-    else if (a == "-o") out = val();
-    else if (a == "--no-header") header = false;
-    else if (a == "-f") sweep = val();
-    else if (a == "-y") cfg.sync_mode = std::atoi(val());
-    else if (a == "-V") cfg.host_validation = true;
-    else if (a == "-h" || a == "--help") { usage(); return 0; }
-    else { usage(); return 2; }
-  }
-  std::vector<xec::BenchmarkConfig> cfgs;
-  if (sweep.empty()) {
-    cfg.ec_params = {k + m, k};
-    cfgs.push_back(cfg);
-  } else {
-    std::ifstream in(sweep);
-    if (!in) {
-      std::fprintf(stderr, "cannot open %s\n", sweep.c_str());
-      return 2;
+  single.block_size = 1u << 20;
+  single.message_size = 256ull * 16 * (1u << 20);
+  single.num_lost_blocks = 1;
+  bool single_mode = false, overwrite = true, to_stdout = false, gpu_selected = false;
+  std::string out_file = "results.csv", sweep;
+
+  int c, idx = 0;
+  while ((c = getopt_long(argc, argv, "hf:ai:w:c:g:s:", long_options, &idx)) != -1) {
+    switch (c) {
+      case 'h': usage(); return EXIT_SUCCESS;
+      case 'f':
+        out_file = optarg;
+        if (out_file.find(".csv") == std::string::npos) fail("Output file must have .csv extension.");
+        break;
+      case 'a': overwrite = false; break;
+      case 'i':
+        base.num_iterations = std::atoi(optarg);
+        if (base.num_iterations <= 0) fail("Number of iterations must be positive.");
+        break;
+      case 'w':
+        base.num_warmup_iterations = std::atoi(optarg);
+        if (base.num_warmup_iterations < 0) fail("Number of warmup iterations must be non-negative.");
+        break;
+      case 'c':
+        for (const auto& a : arg_vector(optarg))
+          fail("Invalid CPU algorithm: " + a + " (this build carries the XOR-EC HIP path only)");
+        break;
+      case 'g':
+        for (const auto& a : arg_vector(optarg)) {
+          if (a != "xorec-hip") fail("Invalid GPU algorithm: " + a);
+          gpu_selected = true;
+        }
+        break;
+      case 's':
+        for (const auto& a : arg_vector(optarg))
+          if (a != "scalar" && a != "sse2" && a != "avx2" && a != "avx512")
+            fail("Invalid SIMD version: " + a);
+        break;
+      case kMessage: single.message_size = parse_size(optarg); single_mode = true; break;
+      case kBlock: single.block_size = parse_size(optarg); single_mode = true; break;
+      case kData: k = parse_size(optarg); single_mode = true; break;
+      case kParity: m = parse_size(optarg); single_mode = true; break;
+      case kLost: single.num_lost_blocks = parse_size(optarg); single_mode = true; break;
+      case kSweep: sweep = optarg; break;
+      case kThreads: base.num_cpu_threads = parse_size(optarg); break;
+      case kDevice: base.device_id = std::atoi(optarg); break;
+      case kSeed: base.seed = parse_size(optarg); break;
+      case kSync: base.sync_mode = std::atoi(optarg); break;
+      case kHostVal: base.host_validation = true; break;
+      case kStdout: to_stdout = true; break;
+      default: usage(); return EXIT_FAILURE;
     }
+  }
+  if (!gpu_selected) fail("No benchmarks selected. Use --gpu xorec-hip to select the benchmark.");
+
+  std::vector<xec::BenchmarkConfig> cfgs;
+  auto with_base = [&](xec::BenchmarkConfig x) {
+    x.num_iterations = base.num_iterations;
+    x.num_warmup_iterations = base.num_warmup_iterations;
+    x.device_id = base.device_id;
+    x.seed = base.seed;
+    x.sync_mode = base.sync_mode;
+    x.host_validation = base.host_validation;
+    return x;
+  };
+  if (!sweep.empty()) {
+    std::ifstream in(sweep);
+    if (!in) fail("cannot open " + sweep);
     std::string line;
     while (std::getline(in, line)) {
       if (line.empty() || line[0] == '#') continue;
       unsigned long long ms, b, kk, mm, l;
       if (std::sscanf(line.c_str(), "%llu %llu %llu %llu %llu", &ms, &b, &kk, &mm, &l) != 5) continue;
-      xec::BenchmarkConfig c = cfg;
-      c.message_size = ms;
-      c.block_size = b;
-      c.ec_params = {kk + mm, kk};
-      c.num_lost_blocks = l;
-      cfgs.push_back(c);
+      xec::BenchmarkConfig x = with_base(base);
+      x.message_size = ms;
+      x.block_size = b;
+      x.ec_params = {kk + mm, kk};
+      x.num_lost_blocks = l;
+      cfgs.push_back(x);
     }
+  } else if (single_mode) {
+    single.ec_params = {k + m, k};
+    cfgs.push_back(with_base(single));
+  } else {
+    cfgs = gpu_sweep(base);
   }
-  for (const auto& c : cfgs) {
-    if (c.num_lost_blocks > xec::parity_blocks(c)) {
+  for (const auto& x : cfgs) {
+    if (x.num_lost_blocks > xec::parity_blocks(x)) {
       // the reference prints and exits (utils.cpp:102-105)
       std::fprintf(stderr, "lost blocks per stripe (%zu) must be <= parity blocks (%zu)\n",
-                   c.num_lost_blocks, xec::parity_blocks(c));
+                   x.num_lost_blocks, xec::parity_blocks(x));
       return 2;
     }
   }
   try {
     std::ofstream f;
     std::ostream* os = &std::cout;
-    if (!out.empty()) {
-      f.open(out, std::ios::app);
+    if (!to_stdout) {
+      f.open(out_file, overwrite ? std::ios::out : std::ios::app);
+      if (!f.is_open()) fail("Error opening file: " + out_file);
       os = &f;
     }
-    if (header) xec::write_csv_header(*os);
+    // CSVReporter (csv_reporter.cpp:11-19): header only when overwriting
+    if (overwrite) xec::write_csv_header(*os);
     int rc = 0;
-    for (const auto& c : cfgs) {
-      xec::RunResult r = xec::run_generic<xec::XorecBenchmarkHip>("XOR-EC (HIP gfx950)", c);
-      xec::write_csv_row(*os, r, c);
+    size_t n = 0;
+    for (const auto& x : cfgs) {
+      xec::RunResult r = xec::run_generic<xec::XorecBenchmarkHip>(kName, x);
+      xec::write_csv_row(*os, r, x);
       os->flush();
+      std::fprintf(stderr, "[%zu/%zu] bs=%zu EC=(%zu/%zu) lost=%zu enc %.1f Gbit/s dec %.1f Gbit/s %s\n",
+                   ++n, cfgs.size(), x.block_size, std::get<0>(x.ec_params),
+                   std::get<1>(x.ec_params), x.num_lost_blocks, r.encode.tp_mean,
+                   r.decode.tp_mean, r.err_msg.c_str());
       if (!r.err_msg.empty()) rc = 1;
     }
     return rc;

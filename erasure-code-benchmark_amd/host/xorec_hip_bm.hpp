@@ -3,8 +3,12 @@
 //
 // Drop-in sibling of the reference's XorecBenchmarkGpuCmp
 // (src/algorithms/xorec_gpu_cmp_bm.{hpp,cpp}): same five virtuals, same batch
-// layout, same pinned host bitmap + device bitmap scratch, one codec call per
-// batch followed by a stream synchronise.  Differences, each a fix:
+// layout, the base class's m_data_buf / m_parity_buf replaced by HBM
+// allocations and m_block_bitmap by pinned host memory (as
+// xorec_gpu_cmp_bm.cpp:6-18 does), a device bitmap scratch, one codec call per
+// batch followed by a stream synchronise.  It overrides the base class's
+// defaults (simulate_data_loss, check_for_corruption, m_write_data_buffer)
+// because they touch buffers that now live in HBM.  Differences, each a fix:
 //   - simulate_data_loss zeroes lost blocks with ONE kernel and synchronises,
 //     instead of per-block cudaMemset calls that drain into the decode timer
 //     (xorec_gpu_cmp_bm.cpp:71-89);
@@ -41,20 +45,18 @@ class XorecBenchmarkHip : public AbstractBenchmark {
   // Last status returned by the codec (xec_status), for diagnostics.
   int last_status() const { return m_last_status; }
 
- private:
-  void write_data_buffer() noexcept;
+ protected:
+  void m_write_data_buffer() noexcept override;
 
+ private:
+  // m_data_buf: device S*k*bs; m_parity_buf: device S*m*bs; m_block_bitmap:
+  // pinned host S*(k+m) (base-class members, replaced in the constructor)
   hipStream_t m_stream = nullptr;
-  uint8_t* m_data = nullptr;        // device, S*k*bs
-  uint8_t* m_parity = nullptr;      // device, S*m*bs
-  uint8_t* m_d_bitmap = nullptr;    // device scratch, S*(k+m)
-  uint8_t* m_d_erase = nullptr;     // device copy of the erasure bitmap
-  uint8_t* m_h_bitmap = nullptr;    // pinned host, S*(k+m)
-  uint8_t* m_h_stage = nullptr;     // pinned host staging (host_validation only)
-  uint32_t* m_d_bad = nullptr;      // device counter of corrupted blocks
+  Buffer m_d_bitmap;   // device scratch for xec_decode, S*(k+m)
+  Buffer m_d_erase;    // device copy of the erasure bitmap for xec_erase
+  Buffer m_h_stage;    // pinned host staging (host_validation only)
+  Buffer m_d_bad;      // device counter of corrupted blocks (4 B)
   bool m_host_validation;
-  uint64_t m_seed;
-  uint64_t m_round = 0;             // bumps per setup(): fresh payload per iteration
   int m_last_status = 0;
 };
 

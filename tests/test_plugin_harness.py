@@ -1,5 +1,8 @@
 """The C++ XorecBenchmarkHip plugin + BM_generic-style harness (bin/xec_bench):
-reference CSV schema, validation-pattern integrity after erase + decode."""
+the reference's CLI contract (benchmark_suite.cpp:102-212), its GPU config
+cross product (get_gpu_configs, :252-277 over bm_config.cpp:3-23), the
+20-column CSV schema (csv_reporter.cpp:11-99), and validation-payload
+integrity after erase + decode."""
 from __future__ import annotations
 
 import csv
@@ -8,7 +11,7 @@ import subprocess
 
 import pytest
 
-from conftest import PKG_DIR
+from conftest import PKG_DIR, ROOT
 
 BENCH = PKG_DIR / "bin" / "xec_bench"
 HEADER = ("name,err_msg,iterations,warmup_iterations,gpu_computation,gpu_blocks,threads_per_block,"
@@ -16,30 +19,106 @@ HEADER = ("name,err_msg,iterations,warmup_iterations,gpu_computation,gpu_blocks,
           "encode_time_ns_stddev,encode_throughput_Gbps,encode_throughput_Gbps_stddev,"
           "decode_time_ns,decode_time_ns_stddev,decode_throughput_Gbps,"
           "decode_throughput_Gbps_stddev").split(",")
+CONFIG_COLS = ["gpu_computation", "gpu_blocks", "threads_per_block", "message_size_B",
+               "block_size_B", "EC", "lost_blocks", "cpu_threads"]
 
 
-def run(*args, timeout=600):
+def run(*args, timeout=600, cwd=None):
     return subprocess.run([str(BENCH), *map(str, args)], capture_output=True, text=True,
-                          timeout=timeout)
+                          timeout=timeout, cwd=cwd)
 
 
-def test_cli_help_and_lost_check():
+def reference_sweep():
+    """The cross product get_gpu_configs builds, in its loop order."""
+    out = []
+    for bs in (1024, 2048, 4096, 8192):
+        for total, data in ((12, 8), (20, 16), (24, 16), (36, 32), (40, 32)):
+            for lost in (0, 1, 2, 4, 8):
+                if lost <= total - data:
+                    out.append((8 << 20, bs, f"({total}/{data})", lost))
+    return out
+
+
+def test_cli_contract_errors():
+    """Argument checks of parse_args (benchmark_suite.cpp:102-212); nothing runs."""
     assert BENCH.exists(), "build with make -C erasure-code-benchmark_amd"
     assert run("--help").returncode == 0
-    r = run("-k", "4", "-m", "1", "-l", "2")
+    r = run("-i", "3")
+    assert r.returncode == 1 and "No benchmarks selected" in r.stderr
+    r = run("-g", "xorec-hip", "-f", "out.txt")
+    assert r.returncode == 1 and ".csv" in r.stderr
+    r = run("-g", "xorec-gpu")
+    assert r.returncode == 1 and "Invalid GPU algorithm" in r.stderr
+    r = run("-c", "xorec", "-g", "xorec-hip")
+    assert r.returncode == 1 and "Invalid CPU algorithm" in r.stderr
+    r = run("-g", "xorec-hip", "-s", "avx1024")
+    assert r.returncode == 1 and "Invalid SIMD version" in r.stderr
+    r = run("-g", "xorec-hip", "-i", "0")
+    assert r.returncode == 1 and "iterations" in r.stderr
+    r = run("-g", "xorec-hip", "-w", "-1")
+    assert r.returncode == 1 and "warmup" in r.stderr
+    r = run("-g", "xorec-hip", "--data", "4", "--parity", "1", "--lost", "2")
     assert r.returncode == 2 and "parity" in r.stderr
 
 
 @pytest.mark.gpu
+def test_reference_gpu_sweep(tmp_path):
+    """`xec_bench -g xorec-hip -f out.csv -i 3`: one clean row per config of the
+    reference's GPU cross product, in its order; config columns equal the
+    reference's own GPU rows where those exist (tools/reference_gpu_rows.csv,
+    the "XOR-EC (GPU Computation)" rows of results/raw/final_results.csv);
+    -a appends without a header."""
+    out = tmp_path / "out.csv"
+    r = run("-g", "xorec-hip", "-f", out, "-i", "3", "-s", "avx2,avx512", timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = list(csv.reader(out.open()))
+    assert rows[0] == HEADER
+    got = [dict(zip(HEADER, x)) for x in rows[1:]]
+    want = reference_sweep()
+    assert [(int(g["message_size_B"]), int(g["block_size_B"]), g["EC"], int(g["lost_blocks"]))
+            for g in got] == want
+    for g in got:
+        assert g["err_msg"] == "", g
+        assert g["iterations"] == "3" and g["warmup_iterations"] == "0"
+        assert float(g["encode_throughput_Gbps"]) > 0
+    ref = [x for x in csv.DictReader(line for line in
+                                     (ROOT / "tools" / "reference_gpu_rows.csv").open()
+                                     if not line.startswith("#"))]
+    by_cfg = {(g["message_size_B"], g["block_size_B"], g["EC"], g["lost_blocks"]): g for g in got}
+    matched = 0
+    for x in ref:
+        key = (x["message_size_B"], x["block_size_B"], x["EC"].strip('"'), x["lost_blocks"])
+        if key in by_cfg:
+            matched += 1
+            assert [by_cfg[key][c] for c in CONFIG_COLS] == \
+                [x[c].strip('"') for c in CONFIG_COLS], key
+    assert matched >= 20
+    # -a: rows appended, no second header
+    r = run("-g", "xorec-hip", "-f", out, "-a", "-i", "2", "--block", "4K", "--data", "16",
+            "--parity", "4", "--lost", "2", "--message", "8M", timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows2 = list(csv.reader(out.open()))
+    assert len(rows2) == len(rows) + 1 and rows2[:len(rows)] == rows
+    # without -a the file is overwritten
+    r = run("-g", "xorec-hip", "-f", out, "-i", "2", "--block", "4K", "--data", "16",
+            "--parity", "4", "--lost", "2", "--message", "8M", timeout=300)
+    assert r.returncode == 0
+    assert len(list(csv.reader(out.open()))) == 2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("args", [
-    ("-s", "64M", "-b", "64K", "-k", "8", "-m", "4", "-l", "4", "-i", "3", "-w", "1"),
-    ("-s", "8M", "-b", "1K", "-k", "32", "-m", "8", "-l", "0", "-i", "3"),
-    ("-s", "32M", "-b", "4K", "-k", "16", "-m", "4", "-l", "2", "-i", "3"),
-    ("-s", "1G", "-b", "1M", "-k", "16", "-m", "1", "-l", "1", "-i", "2", "-w", "1"),
-    ("-s", "64M", "-b", "8K", "-k", "16", "-m", "4", "-l", "3", "-i", "2", "-V"),
+    ("--message", "64M", "--block", "64K", "--data", "8", "--parity", "4", "--lost", "4",
+     "-i", "3", "-w", "1"),
+    ("--message", "8M", "--block", "1K", "--data", "32", "--parity", "8", "--lost", "0", "-i", "3"),
+    ("--message", "32M", "--block", "4K", "--data", "16", "--parity", "4", "--lost", "2", "-i", "3"),
+    ("--message", "1G", "--block", "1M", "--data", "16", "--parity", "1", "--lost", "1", "-i", "2",
+     "-w", "1"),
+    ("--message", "64M", "--block", "8K", "--data", "16", "--parity", "4", "--lost", "3", "-i", "2",
+     "--host-validation"),
 ])
 def test_harness_rows_clean(args):
-    r = run(*args, "-r", "7")
+    r = run("-g", "xorec-hip", "--stdout", *args, "--seed", "7")
     assert r.returncode == 0, r.stderr + r.stdout
     rows = list(csv.reader(io.StringIO(r.stdout)))
     assert rows[0] == HEADER

@@ -45,8 +45,9 @@ def main():
         for c in cfgs:
             f.write(" ".join(map(str, c)) + "\n")
         sweep = f.name
-    p = subprocess.run([str(BENCH), "-f", sweep, "-i", str(args.iters), "-w", str(args.warmup),
-                        "-r", "1896"], capture_output=True, text=True, timeout=1500)
+    p = subprocess.run([str(BENCH), "-g", "xorec-hip", "--sweep", sweep, "-i", str(args.iters),
+                        "-w", str(args.warmup), "--seed", "1896", "--stdout"],
+                       capture_output=True, text=True, timeout=1500)
     if p.returncode != 0:
         sys.exit(f"xec_bench failed rc={p.returncode}: {p.stderr}\n{p.stdout[-2000:]}")
     if args.csv_out:
