@@ -151,19 +151,32 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
                                                                            : XEC_DEVICE_ERROR;
 }
 
+// Bitmaps from this size on are copied to the device BEFORE the host scan, so
+// the scan (~1.1 ns per stripe, 75 us for config 4's 65,536 stripes) runs
+// while the transfer does and the synchronous caller waits for
+// max(scan, copy) + kernel instead of their sum (tools/scan_cost.py,
+// profiles/r02b, r02c).  Smaller bitmaps keep the scan first, so a batch that
+// needs no recovery queues no device work at all.
+constexpr size_t kCopyFirstBitmapBytes = 256u << 10;
+
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k, size_t m,
                       const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream) {
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
+  const size_t bitmap_bytes = S * (k + m);
+  const bool copy_first = bitmap_bytes >= kCopyFirstBitmapBytes;
+  if (copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
+                                   stream) != hipSuccess)
+    return XEC_DEVICE_ERROR;
   int needs = 0;
   uint64_t lost = 0;
   st = xec_scan_bitmap(h_bitmap, S, k, m, &needs, &lost);
-  if (st != XEC_SUCCESS) return st;
+  if (st != XEC_SUCCESS) return st;  // nothing but the scratch copy was queued
   if (!needs) return XEC_SUCCESS;
-  if (hipMemcpyAsync(d_bitmap, h_bitmap, S * (k + m), hipMemcpyHostToDevice, stream) !=
-      hipSuccess)
+  if (!copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
+                                    stream) != hipSuccess)
     return XEC_DEVICE_ERROR;
   // class tiles: one reduction per tile, so the encode's residency table
   const bool cls = use_class_tiles(S, m, lost);

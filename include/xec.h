@@ -67,15 +67,19 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * h_bitmap: S*(k+m) bytes of host memory (pinned for an asynchronous copy);
  * d_bitmap: S*(k+m) bytes of device scratch owned by the caller.
  * Host checks follow the reference: XEC_DECODE_FAILURE if ANY stripe is
- * unrecoverable (is_recoverable, xorec_utils.hpp:160-175) and then nothing is
- * touched; XEC_SUCCESS with no device work if no stripe needs recovery
+ * unrecoverable (is_recoverable, xorec_utils.hpp:160-175) and then no data is
+ * touched; XEC_SUCCESS without a kernel if no stripe needs recovery
  * (require_recovery, xorec_utils.hpp:144-149).  Otherwise h_bitmap is copied
  * to d_bitmap on `stream` and every lost data block is rebuilt:
  *   data[c][i] = parity[c][i%m] ^ XOR_{l%m == i%m, l != i} data[c][l].
  * Lost parity is not regenerated.  Parity is READ-ONLY here, as in the CPU
  * decode (xorec.cpp:62-111) -- deliberately unlike the reference GPU decode,
  * which folds all data into parity (xorec_gpu_cmp.cu:94-102).  The content of
- * lost data blocks on entry is irrelevant (no zeroing pre-condition). */
+ * lost data blocks on entry is irrelevant (no zeroing pre-condition).
+ * For bitmaps of 256 KiB and more (S*(k+m) bytes) the copy into d_bitmap is
+ * queued before the host scan, so the two overlap; d_bitmap is then written
+ * whatever the verdict (it is scratch).  h_bitmap must stay unchanged until
+ * the stream has passed the call, as for any asynchronous copy. */
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                       size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream);
 

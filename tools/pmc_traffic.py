@@ -12,7 +12,12 @@ WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports exactly half of a wide
 (16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE is exact for
 16-B-per-lane streaming stores.  Both our kernels use only 16-B loads/stores.
 
-    python tools/pmc_traffic.py <tag> <workload> [--bench-log FILE]
+    python tools/pmc_traffic.py <tag> <workload> [lost]
+
+<workload> is a bench.py workload name or a custom "k,m,bs,S" shape; [lost]
+(default 1) = lost data blocks per stripe of the profiled decode (bench.py
+--lost), which scales the decode's algorithmic bytes.  traffic_<workload>.json
+is written for named workloads only.
 """
 from __future__ import annotations
 
@@ -39,6 +44,7 @@ def per_kernel(csv_path: Path) -> dict[str, list[float]]:
 
 def main():
     tag, workload = sys.argv[1], sys.argv[2]
+    lost = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     src = ROOT / "gpurun_out" / f"prof_{tag}"
     dst = ROOT / "profiles"
     dst.mkdir(exist_ok=True)
@@ -47,10 +53,11 @@ def main():
     write = per_kernel(src / "pmc_WRITE_SIZE" / "pmc_counter_collection.csv")
     stats = {short(r["Name"]): r for r in csv.DictReader(open(src / "trace" / "kt_kernel_stats.csv"))}
 
-    from bench import WORKLOADS, algorithmic_bytes
-    k, m, bs, S, _ = WORKLOADS[workload]
+    from bench import WORKLOADS, algorithmic_bytes, workload_shape
+    k, m, bs, S, _ = workload_shape(workload)
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
-    algo = {"xec::encode_kernel": b_enc, "xec::decode_kernel": b_dec}
+    algo = {"xec::encode_kernel": b_enc, "xec::decode_kernel": b_dec * lost,
+            "xec::decode_class_kernel": b_dec * lost}
 
     kernels = {}
     for name in sorted(set(fetch) & set(write)):
@@ -73,15 +80,16 @@ def main():
             "achieved_GBps_algorithmic": round(algo[base] / avg_ns, 1) if avg_ns else None,
         }
     out = {"tag": tag, "workload": workload, "k": k, "m": m, "block_bytes": bs, "stripes": S,
+           "lost_per_stripe": lost,
            "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE halves 16-B streams)",
            "kernels": kernels}
     (dst / f"{tag}_pmc.json").write_text(json.dumps(out, indent=1) + "\n")
     enc = [v for n, v in kernels.items() if n.startswith("xec::encode_kernel")]
-    if enc:
+    if enc and workload in WORKLOADS:
         traffic = {"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)",
                    "encode_hbm_bytes_per_launch": enc[0]["hbm_bytes_per_launch"],
                    "encode_algorithmic_bytes_per_launch": enc[0]["algorithmic_bytes_per_launch"]}
-        dec = [v for n, v in kernels.items() if n.startswith("xec::decode_kernel")]
+        dec = [v for n, v in kernels.items() if n.startswith("xec::decode")]
         if dec:
             traffic["decode_hbm_bytes_per_launch"] = dec[0]["hbm_bytes_per_launch"]
         (dst / f"traffic_{workload}.json").write_text(json.dumps(traffic, indent=1) + "\n")

@@ -34,6 +34,11 @@ def main():
     ap.add_argument("--lost", default="", help="comma list; default 1, m/2, m (distinct)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--occ", default="",
+                    help="comma list of xec_set_occupancy values (1..8) to also time class "
+                         "tiles at (variants class@oN); default: automatic residency only")
+    ap.add_argument("--only-class", action="store_true",
+                    help="time class tiles (and their --occ variants) and encode only")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -65,14 +70,23 @@ def main():
             h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
             d_bm = h_bm.to("cuda")
             scratch = [torch.empty_like(d_bm) for _ in range(3)]
-            variants = {"stripe": 1, "class": 2, "auto": 0} if m > 1 else {"stripe": 1}
+            # variant -> (tiling, occupancy); occupancy None = automatic
+            variants = ({"stripe": (1, None), "class": (2, None), "auto": (0, None)} if m > 1
+                        else {"stripe": (1, None)})
+            if args.only_class and m > 1:
+                variants = {"class": (2, None)}
+            for o in (int(x) for x in args.occ.split(",") if x):
+                variants[f"class@o{o}"] = (2 if m > 1 else 1, o)
             times = {v: [] for v in variants}
             times["encode"] = []
             it = 0
             for _ in range(args.rounds):
                 for v, t in list(variants.items()) + [("encode", None)]:
                     if t is not None:
-                        assert xec.set_decode_tiling(t) == 0
+                        assert xec.set_decode_tiling(t[0]) == 0
+                        assert xec.set_occupancy(t[1] or 0) == 0
+                    else:
+                        assert xec.set_occupancy(0) == 0
                     evs = [(torch.cuda.Event(enable_timing=True),
                             torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
                     for i in range(args.iters):
@@ -90,13 +104,15 @@ def main():
             fresh = torch.empty_like(sets[0][0])
             ok = {}
             for v, t in variants.items():
-                assert xec.set_decode_tiling(t) == 0
+                assert xec.set_decode_tiling(t[0]) == 0
+                assert xec.set_occupancy(t[1] or 0) == 0
                 d, p = sets[0]
                 assert xec.erase(d, p, S, bs, k, m, d_bm, stream) == 0
                 assert xec.decode(d, p, S, bs, k, m, h_bm, scratch[0], stream) == 0
                 assert xec.fill_splitmix64(fresh, S, k * bs, 1000, stream) == 0
                 ok[v] = bool(torch.equal(fresh, d))
             assert xec.set_decode_tiling(0) == 0
+            assert xec.set_occupancy(0) == 0
             del fresh
             b_dec = b_dec1 * lost
             row = {"k": k, "m": m, "bs": bs, "S": S, "lost_per_stripe": lost,
