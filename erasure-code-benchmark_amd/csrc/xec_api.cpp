@@ -278,6 +278,12 @@ xec_status xec_set_decode_tiling(int tiling) {
   return XEC_SUCCESS;
 }
 
+xec_status xec_set_validate_kernel(int mode) {
+  if (mode < 0 || mode > 2) return XEC_INVALID_SIZE;
+  xec::g_validate_mode = mode;
+  return XEC_SUCCESS;
+}
+
 const char* xec_status_string(xec_status s) {
   switch (s) {
     case XEC_SUCCESS: return "Success";

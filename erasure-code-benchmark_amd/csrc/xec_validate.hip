@@ -5,11 +5,27 @@
 // (u32, crc = rotl(crc,3) + byte, seeded with the length) at 0
 // (src/utils/utils.cpp:35-97), generated and validated on the host with a
 // full device<->host copy each iteration (xorec_gpu_cmp_bm.cpp:25-37,91-104).
-// Here both run where the data lives.  The checksum is a strictly sequential
-// chain, so the unit of parallelism is the block: one lane owns one block and
-// walks it with 16-byte accesses (generation: PCG32, utils.cpp:17-32, with
+// Here both run where the data lives (generation: PCG32, utils.cpp:17-32, with
 // state RANDOM_SEED + seed + block, stream 1; the wall-clock seed of the
 // reference is replaced by an explicit one).
+//
+// Two kernel shapes, same results:
+//  * lane per block (serial_*): one lane walks a whole block.  Used for the
+//    pattern when there are enough blocks to fill the chip (>= kLaneBlocks),
+//    and whenever the block does not tile into 128-byte segments.
+//  * G lanes per block (wave_*<G>, 64/G blocks per wave): the lanes split the
+//    checksum chain.  Past a serial head (bytes 8..127), a block is walked in
+//    windows of G*128 bytes, lane j owning the 128 contiguous bytes at
+//    window + 128 j.  rotl3 is multiplication by 8 modulo 2^32-1 and
+//    8^128 == 1 there, so a lane's segment maps a start state x to x + S
+//    (ones'-complement) where S is the segment's Horner sum -- unless an
+//    addition carried out of 32 bits, which the ones'-complement form cannot
+//    see (probability ~2^-25 per byte).  Each lane takes the speculated start
+//    W + S_0 + ... + S_{j-1} (a scan over the group), runs the true chain from
+//    it and checks that it ends where lane j+1 starts.  Lane 0 starts from the
+//    exact state, so if every check passes every lane was exact; otherwise
+//    the window is redone lane after lane.  Exact by construction; modelled
+//    in Python in tests/crc_model.py, tests/test_crc_split.py.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -42,8 +58,34 @@ __device__ __forceinline__ uint32_t rotl3(uint32_t x) { return (x << 3) | (x >> 
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void pattern_kernel(uint8_t* data, uint64_t nblocks, uint64_t bs,
-                                                      uint64_t seed) {
+// x + byte Q of w in one v_add_u32 with an SDWA byte select.  Written as asm
+// so the byte extracts cannot be hoisted out of the chain (the scheduler would
+// otherwise keep all 128 extracted bytes live, 120+ VGPRs).
+#define XEC_ADD_BYTE(Q)                                                                   \
+  __device__ __forceinline__ uint32_t add_byte##Q(uint32_t x, uint32_t w) {              \
+    uint32_t r;                                                                          \
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "  \
+        "src1_sel:BYTE_" #Q                                                              \
+        : "=v"(r)                                                                        \
+        : "v"(x), "v"(w));                                                               \
+    return r;                                                                            \
+  }
+XEC_ADD_BYTE(0)
+XEC_ADD_BYTE(1)
+XEC_ADD_BYTE(2)
+XEC_ADD_BYTE(3)
+#undef XEC_ADD_BYTE
+
+// The reference chain (utils.cpp:53-55) over one little-endian word.
+__device__ __forceinline__ uint32_t word_chain(uint32_t x, uint32_t w) {
+  x = add_byte0(rotl3(x), w);
+  x = add_byte1(rotl3(x), w);
+  x = add_byte2(rotl3(x), w);
+  return add_byte3(rotl3(x), w);
+}
+
+__global__ __launch_bounds__(256) void serial_pattern_kernel(uint8_t* data, uint64_t nblocks,
+                                                             uint64_t bs, uint64_t seed) {
   const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= nblocks) return;
   uint8_t* blk = data + b * bs;
@@ -89,8 +131,9 @@ __global__ __launch_bounds__(256) void pattern_kernel(uint8_t* data, uint64_t nb
   }
 }
 
-__global__ __launch_bounds__(256) void validate_kernel(const uint8_t* data, uint64_t nblocks,
-                                                       uint64_t bs, uint32_t* bad) {
+__global__ __launch_bounds__(256) void serial_validate_kernel(const uint8_t* data,
+                                                              uint64_t nblocks, uint64_t bs,
+                                                              uint32_t* bad) {
   const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= nblocks) return;
   const uint8_t* blk = data + b * bs;
@@ -113,7 +156,7 @@ __global__ __launch_bounds__(256) void validate_kernel(const uint8_t* data, uint
       for (; i < bs; i += 16) {
         const u32x4 g = *reinterpret_cast<const u32x4*>(blk + i);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) crc = rotl3(crc) + ((g[q >> 2] >> (8 * (q & 3))) & 0xffu);
+        for (int c = 0; c < 4; ++c) crc = word_chain(crc, g[c]);
       }
     } else {
       for (; i < bs; ++i) crc = rotl3(crc) + blk[i];
@@ -123,13 +166,244 @@ __global__ __launch_bounds__(256) void validate_kernel(const uint8_t* data, uint
   if (!ok) atomicAdd(bad, 1u);
 }
 
+// ---- G lanes per block (a wave holds 64/G blocks) -----------------------------
+
+constexpr int kSeg = 128;                     // bytes per lane per window
+constexpr uint64_t kLaneBlocks = 1ull << 18;  // pattern: lane per block fills the chip from here
+
+__device__ __forceinline__ uint32_t oc_add(uint32_t a, uint32_t b) {  // mod 2^32-1
+  const uint32_t s = a + b;
+  return s + (uint32_t)(s < a);
+}
+__device__ __forceinline__ uint32_t rotl12(uint32_t x) { return (x << 12) | (x >> 20); }
+
+struct Segment {
+  u32x4 g[kSeg / 16];
+};
+
+// Horner sum of the segment's bytes, sum 8^(kSeg-1-n) v_n mod 2^32-1, four
+// bytes (one factor 8^4 = rotl12) per step.
+__device__ __forceinline__ uint32_t seg_horner(const Segment& sg) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int t = 0; t < kSeg / 16; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t w = sg.g[t][c];
+      // 8^3 b0 + 8^2 b1 + 8 b2 + b3 = 8 * dot4(bytes, (64, 8, 1, 0)) + b3
+      const uint32_t v = (__builtin_amdgcn_udot4(w, 0x00010840u, 0u, false) << 3) + (w >> 24);
+      s = oc_add(rotl12(s), v);
+    }
+  return s;
+}
+
+// ... and the reference chain over the segment from state x.
+__device__ __forceinline__ uint32_t seg_chain(uint32_t x, const Segment& sg) {
+#pragma unroll
+  for (int t = 0; t < kSeg / 16; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x = word_chain(x, sg.g[t][c]);
+  return x;
+}
+
+// Advance the checksum state W over one window of G segments; every lane of
+// the group returns the state after the window.  `sub` = lane within the
+// group; `active` = the lane's segment lies inside the block (inactive lanes
+// are the group's tail and act as the identity).
+template <int G>
+__device__ uint32_t window_crc(uint32_t W, const Segment& sg, bool active, int sub) {
+  const uint32_t S = active ? seg_horner(sg) : 0u;
+  uint32_t incl = S;
+#pragma unroll
+  for (int d = 1; d < G; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d, G);
+    if (sub >= d) incl = oc_add(incl, t);
+  }
+  const uint32_t excl = __shfl_up(incl, 1, G);
+  const uint32_t start = sub == 0 ? W : oc_add(W, excl);
+  const uint32_t end = active ? seg_chain(start, sg) : start;
+  const uint32_t next_start = __shfl_down(start, 1, G);
+  if (__ballot(sub < G - 1 && end != next_start) == 0) return __shfl(end, G - 1, G);
+  // a carry somewhere in the wave: every group walks its window lane after
+  // lane from its exact state
+  uint32_t cur = W;
+  for (int j = 0; j < G; ++j) {
+    const uint32_t e = active ? seg_chain(cur, sg) : cur;
+    cur = __shfl(e, j, G);
+  }
+  return cur;
+}
+
+// Chain over the head, bytes 8..kSeg-1 (every lane of the group, same addresses).
+__device__ __forceinline__ uint32_t head_crc(const uint8_t* blk, uint32_t crc) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(blk);
+  for (int i = 2; i < kSeg / 4; ++i) crc = word_chain(crc, w[i]);
+  return crc;
+}
+
+// Requires bs % kSeg == 0, bs >= 2 kSeg, 16-B aligned blocks; G >= the
+// segments per block past the head, or 64.  Windows of G*kSeg bytes.
+template <int G>
+__global__ __launch_bounds__(64) void wave_validate_kernel(const uint8_t* data, uint64_t nblocks,
+                                                           uint64_t bs, uint32_t* bad) {
+  constexpr int kBpw = 64 / G;  // blocks per wave
+  constexpr uint64_t kWin = (uint64_t)G * kSeg;
+  const int sub = threadIdx.x % G;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * kBpw; b0 < nblocks; b0 += (uint64_t)gridDim.x * kBpw) {
+    const uint64_t b = b0 + threadIdx.x / G;
+    const bool valid = b < nblocks;
+    const uint8_t* blk = data + (valid ? b : b0) * bs;
+    auto load = [&](Segment& sg, uint64_t base) {
+      const uint64_t off = base + (uint64_t)sub * kSeg;
+      const u32x4* src = reinterpret_cast<const u32x4*>(blk + (valid && off < bs ? off : 0));
+#pragma unroll
+      for (int t = 0; t < kSeg / 16; ++t) sg.g[t] = src[t];
+    };
+    Segment cur;
+    load(cur, kSeg);
+    uint32_t W = head_crc(blk, (uint32_t)bs);
+    if constexpr (G < 64) {  // G covers the block: one window
+      W = window_crc<G>(W, cur, valid && kSeg + (uint64_t)sub * kSeg < bs, sub);
+    } else {  // the next window's segment is in flight while this one is reduced
+      Segment nxt;
+      for (uint64_t base = kSeg; base < bs; base += kWin) {
+        if (base + kWin < bs) load(nxt, base + kWin);
+        W = window_crc<G>(W, cur, base + (uint64_t)sub * kSeg < bs, sub);
+        cur = nxt;
+      }
+    }
+    if (valid && sub == 0) {
+      const uint32_t* hdr = reinterpret_cast<const uint32_t*>(blk);
+      if (!(hdr[1] == (uint32_t)bs && hdr[0] == W)) atomicAdd(bad, 1u);
+    }
+  }
+}
+
+// PCG32 advance by `delta` steps (log-time LCG jump).
+__device__ uint64_t pcg_advance(uint64_t state, uint64_t delta, uint64_t inc) {
+  uint64_t acc_mult = 1, acc_plus = 0, cur_mult = kPcgMul, cur_plus = inc;
+  while (delta) {
+    if (delta & 1) {
+      acc_mult *= cur_mult;
+      acc_plus = acc_plus * cur_mult + cur_plus;
+    }
+    cur_plus = (cur_mult + 1) * cur_plus;
+    cur_mult *= cur_mult;
+    delta >>= 1;
+  }
+  return acc_mult * state + acc_plus;
+}
+
+// Same layout as wave_validate_kernel; each lane generates its segment of a
+// window from the PCG state jumped to the segment's first byte (byte i of a
+// block is output number i-8).
+template <int G>
+__global__ __launch_bounds__(64) void wave_pattern_kernel(uint8_t* data, uint64_t nblocks,
+                                                          uint64_t bs, uint64_t seed) {
+  constexpr int kBpw = 64 / G;
+  constexpr uint64_t kWin = (uint64_t)G * kSeg;
+  const int sub = threadIdx.x % G;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * kBpw; b0 < nblocks; b0 += (uint64_t)gridDim.x * kBpw) {
+    const uint64_t b = b0 + threadIdx.x / G;
+    const bool valid = b < nblocks;
+    uint8_t* blk = data + (valid ? b : b0) * bs;
+    Pcg rng(kRandomSeed + seed + b, 1);
+    const uint64_t state0 = rng.state;
+    uint32_t W = (uint32_t)bs;
+    for (int i = 2; i < kSeg / 4; ++i) {  // head, bytes 8..kSeg-1
+      uint32_t x = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x |= (rng.next() & 0xffu) << (8 * q);
+      W = word_chain(W, x);
+      if (valid && sub == 0) reinterpret_cast<uint32_t*>(blk)[i] = x;
+    }
+    rng.state = pcg_advance(state0, (uint64_t)kSeg - 8 + (uint64_t)sub * kSeg, rng.inc);
+    for (uint64_t base = kSeg; base < bs; base += kWin) {
+      const uint64_t off = base + (uint64_t)sub * kSeg;
+      const bool active = valid && off < bs;
+      Segment sg;
+#pragma unroll
+      for (int t = 0; t < kSeg / 16; ++t) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x |= (rng.next() & 0xffu) << (8 * q);
+          asm volatile("" : "+v"(x));  // in order: keeps the scheduler from holding 128 PCG states
+          sg.g[t][c] = x;
+        }
+      }
+      if (active) {
+        u32x4* dst = reinterpret_cast<u32x4*>(blk + off);
+#pragma unroll
+        for (int t = 0; t < kSeg / 16; ++t) dst[t] = sg.g[t];
+      }
+      W = window_crc<G>(W, sg, active, sub);
+      if (base + kWin < bs) rng.state = pcg_advance(rng.state, kWin - kSeg, rng.inc);
+    }
+    if (valid && sub == 0) {
+      reinterpret_cast<uint32_t*>(blk)[0] = W;
+      reinterpret_cast<uint32_t*>(blk)[1] = (uint32_t)bs;
+    }
+  }
+}
+
+// Lanes per block: segments past the head, rounded up to a power of two, at
+// most a wave.  0 = the block does not tile into segments (lane kernels).
+int group_lanes(uint64_t bs) {
+  if (bs < 2 * kSeg || bs % kSeg != 0) return 0;
+  const uint64_t segs = bs / kSeg - 1;
+  int g = 1;
+  while (g < 64 && (uint64_t)g < segs) g <<= 1;
+  return g;
+}
+
+template <template <int> class K, typename... A>
+void launch_grouped(int g, uint64_t nblocks, hipStream_t s, A... args) {
+  const uint64_t waves = (nblocks + (64 / g) - 1) / (64 / g);
+  const uint32_t grid = grid_for(waves, 0, 64);
+  switch (g) {
+    case 1: K<1>::launch(grid, s, args...); break;
+    case 2: K<2>::launch(grid, s, args...); break;
+    case 4: K<4>::launch(grid, s, args...); break;
+    case 8: K<8>::launch(grid, s, args...); break;
+    case 16: K<16>::launch(grid, s, args...); break;
+    case 32: K<32>::launch(grid, s, args...); break;
+    default: K<64>::launch(grid, s, args...); break;
+  }
+}
+
+template <int G>
+struct ValidateK {
+  static void launch(uint32_t grid, hipStream_t s, const uint8_t* d, uint64_t n, uint64_t bs,
+                     uint32_t* bad) {
+    wave_validate_kernel<G><<<grid, 64, 0, s>>>(d, n, bs, bad);
+  }
+};
+template <int G>
+struct PatternK {
+  static void launch(uint32_t grid, hipStream_t s, uint8_t* d, uint64_t n, uint64_t bs,
+                     uint64_t seed) {
+    wave_pattern_kernel<G><<<grid, 64, 0, s>>>(d, n, bs, seed);
+  }
+};
+
 }  // namespace
+
+int g_validate_mode = 0;  // 0 auto, 1 lane per block, 2 wave per block (xec_set_validate_kernel)
 
 hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t seed,
                           hipStream_t s) {
   if (nblocks == 0) return hipSuccess;
-  pattern_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(static_cast<uint8_t*>(d_data),
-                                                                  nblocks, bs, seed);
+  uint8_t* d = static_cast<uint8_t*>(d_data);
+  const int g = group_lanes(bs);
+  // The lane kernel wins once there are lanes enough for every block: its PCG
+  // walk needs no jumps (config 4, 2 M blocks: 6.2 vs 14.6 ms, profiles/r02e).
+  const bool grouped = g && (g_validate_mode == 2 || (g_validate_mode == 0 && nblocks < kLaneBlocks));
+  if (grouped)
+    launch_grouped<PatternK>(g, nblocks, s, d, nblocks, bs, seed);
+  else
+    serial_pattern_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(d, nblocks, bs, seed);
   return hipGetLastError();
 }
 
@@ -137,8 +411,15 @@ hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, ui
                            hipStream_t s) {
   if (hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
   if (nblocks == 0) return hipSuccess;
-  validate_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(
-      static_cast<const uint8_t*>(d_data), nblocks, bs, d_bad);
+  const uint8_t* d = static_cast<const uint8_t*>(d_data);
+  const int g = group_lanes(bs);
+  // Grouped lanes read each segment with 16-B loads a lane walks in order;
+  // the lane kernel's strided walk loses even with 2 M blocks (profiles/r02e).
+  if (g && g_validate_mode != 1)
+    launch_grouped<ValidateK>(g, nblocks, s, d, nblocks, bs, d_bad);
+  else
+    serial_validate_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(d, nblocks, bs,
+                                                                            d_bad);
   return hipGetLastError();
 }
 

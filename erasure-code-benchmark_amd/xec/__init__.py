@@ -7,12 +7,14 @@ multi-GPU partitioning helpers; it never computes parity itself.
 from ._lib import EXPORTED, LIB_PATH, Status, XecLibraryError, lib
 from .codec import (Pipeline, build_info, check_args, check_bitmap, decode, decode_device,
                     encode, erase, fill_splitmix64, init, set_decode_tiling, set_launch,
-                    set_occupancy, status_string, validate_blocks, write_validation_pattern)
+                    set_occupancy, set_validate_kernel, status_string, validate_blocks,
+                    write_validation_pattern)
 from .partition import stripe_range
 
 __all__ = [
     "EXPORTED", "LIB_PATH", "Pipeline", "Status", "XecLibraryError", "lib", "build_info",
     "check_args", "check_bitmap", "decode", "decode_device", "encode", "erase",
     "fill_splitmix64", "init", "set_decode_tiling", "set_launch", "set_occupancy",
-    "status_string", "stripe_range", "validate_blocks", "write_validation_pattern",
+    "set_validate_kernel", "status_string", "stripe_range", "validate_blocks",
+    "write_validation_pattern",
 ]

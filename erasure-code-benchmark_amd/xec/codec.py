@@ -110,6 +110,12 @@ def set_decode_tiling(tiling: int = 0) -> Status:
     return Status(lib().xec_set_decode_tiling(tiling))
 
 
+def set_validate_kernel(mode: int = 0) -> Status:
+    """xec_set_validate_kernel; 0 = automatic (default), 1 = lane per block,
+    2 = wave per block (identical results)."""
+    return Status(lib().xec_set_validate_kernel(mode))
+
+
 def status_string(st: int) -> str:
     return lib().xec_status_string(int(st)).decode()
 

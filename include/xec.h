@@ -170,6 +170,17 @@ xec_status xec_set_occupancy(int waves_per_simd);
  * only the speed differs.  XEC_INVALID_SIZE outside 0..2. */
 xec_status xec_set_decode_tiling(int tiling);
 
+/* Tuning / diagnostics (no reference counterpart): kernel shape of
+ * xec_write_validation_pattern / xec_validate_blocks.  Grouped: the checksum
+ * chain of a block is split across G lanes (G = its 128-byte segments past
+ * the first 128 bytes, rounded up to a power of two, at most 64; 64/G blocks
+ * per wave); needs bs % 128 == 0 and bs >= 256.  Lane: one lane walks a whole
+ * block.  0 = automatic (default): validation grouped wherever bs allows it;
+ * the pattern grouped below 2^18 blocks, lane per block from there.
+ * 1 = always lane per block, 2 = grouped wherever bs allows it.  Results are
+ * identical.  XEC_INVALID_SIZE outside 0..2. */
+xec_status xec_set_validate_kernel(int mode);
+
 /* ---- host-in / host-out pipeline --------------------
  * The MI355X analogue of the reference's GPU-memory / unified-memory variants
  * (src/algorithms/xorec_gpu_ptr_bm.cpp:17-65, xorec_unified_ptr_bm.cpp:15-86,
