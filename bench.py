@@ -540,7 +540,11 @@ def run_rank(args):
 
     # every rank's (elapsed, encode ms, decode ms, failed, stripes); rank 0 reports
     # the max time over ranks and each rank's own rates
-    mine = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0, float(S)],
+    # which device this rank ran on (PCI bus id), so the line shows N distinct GPUs
+    bus = -1.0
+    if devname == "cuda":
+        bus = float(getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", -1))
+    mine = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0, float(S), float(dev), bus],
                         dtype=torch.float64, device=coll_dev)
     if use_dist:
         rows = [torch.zeros_like(mine) for _ in range(world)]
@@ -631,7 +635,8 @@ def run_rank(args):
                                                / (r[1] * 1e-3) / 1e9, 1) if r[1] else None,
                           "decode_GBps": round(args.lost * algorithmic_bytes(int(r[4]), k, m, bs)[1]
                                                / (r[2] * 1e-3) / 1e9, 1) if r[2] else None,
-                          "elapsed_ms": round(r[0] * 1e3, 3)} for i, r in enumerate(rows)],
+                          "elapsed_ms": round(r[0] * 1e3, 3), "device": int(r[5]),
+                          "pci_bus_id": int(r[6])} for i, r in enumerate(rows)],
             # per-launch HIP-event statistics on rank 0 (median with stddev)
             "launch_stats_rank0": {
                 n: {"mean_ms": round(statistics.fmean(v), 4),

@@ -36,6 +36,7 @@ def test_launcher_plain_command(n):
     assert out["config"]["stripes_total"] == 5 * n
     assert [r["rank"] for r in out["per_rank"]] == list(range(n))
     assert all(r["stripes"] == 5 for r in out["per_rank"])
+    assert [r["device"] for r in out["per_rank"]] == [0] * n  # CPU stand-ins: one "device"
     assert out["verified"] is True
     assert out["data"].startswith("CPU REHEARSAL")
     assert out["cpu_baseline"] is None  # the CPU leg is N=1 only
