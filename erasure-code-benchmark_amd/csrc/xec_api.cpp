@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <mutex>
+#include <vector>
 
 #include "xec_internal.h"
 #include "xec_kernels.h"
@@ -26,7 +28,7 @@ std::atomic<int> g_max_grid{0};
 std::atomic<int> g_nt{0};
 std::atomic<int> g_threads{0};
 std::atomic<int> g_occupancy{0};  // xec_set_occupancy: waves per SIMD, 0 = automatic
-std::atomic<int> g_decode_tiling{0};  // xec_set_decode_tiling: 0 auto, 1 stripe, 2 class
+std::atomic<int> g_decode_tiling{0};  // xec_set_decode_tiling: 0 auto, 1 stripe, 2 class, 3 list
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
@@ -77,10 +79,12 @@ int decode_auto_occupancy(uint64_t nm, uint64_t lost_data, uint64_t S) {
   return work >= 8 ? 2 : work >= 4 ? 4 : 0;
 }
 
-// Decode tiling (xec_kernels.hip): stripe tiles run one class reduction per
-// lost data block of their stripe, back to back; class tiles are encode's
-// tiles, one reduction each, but a class without a loss leaves its tiles idle.
-// Measured in one process on both tilings (tools/tiling_ab.py,
+// Decode tiling (xec_kernels.hip).  List tiles (the default where the list
+// fits, below) give every lost data block its own tiles: one reduction each,
+// none idle, whatever the spread of the losses.  Otherwise, stripe tiles run
+// one class reduction per lost data block of their stripe, back to back;
+// class tiles are encode's tiles, one reduction each, but a class without a
+// loss leaves its tiles idle.  Measured in one process on both (tools/tiling_ab.py,
 // profiles/r02a/tiling_ab.json; 16+2, 8+2 x 1 MiB, 16+4, 16+8, 32+8 x 64 KiB at
 // 1, m/2 and m losses per stripe): class tiles win once more than one block
 // per stripe AND at least half of the classes are lost (+3 to +9 % with every
@@ -91,7 +95,78 @@ bool use_class_tiles(uint64_t S, uint64_t m, uint64_t lost_data) {
   const int t = g_decode_tiling.load(std::memory_order_relaxed);
   if (m <= 1 || t == 1) return false;
   if (t == 2) return true;
-  return lost_data > S && 2 * lost_data >= S * m;
+  return lost_data > S && 2 * lost_data >= S * m;  // automatic (0, or 3 without a list)
+}
+
+// ---- work-list staging -------------------------------------------------------
+// The work list is written by the host scan into pinned host memory and copied
+// into the caller's d_bitmap scratch on the stream.  A staging buffer is
+// reused once the copy queued from it has run (its event); buffers are kept
+// for the life of the process (a copy may still be queued when a call
+// returns), at most kMaxStaging per process unless every one is in use.
+struct Staging {
+  void* host = nullptr;
+  size_t cap = 0;
+  int device = -1;
+  hipEvent_t done = nullptr;
+  bool busy = false;
+};
+constexpr size_t kMaxStaging = 64;
+std::mutex g_stage_mu;
+std::vector<Staging*> g_stage;
+
+Staging* stage_acquire(size_t bytes, int dev) {
+  std::unique_lock<std::mutex> lk(g_stage_mu);
+  Staging* pick = nullptr;
+  for (Staging* st : g_stage) {
+    if (st->busy || st->device != dev || st->cap < bytes) continue;
+    if (hipEventQuery(st->done) != hipSuccess) continue;  // a queued copy still reads it
+    if (pick == nullptr || st->cap < pick->cap) pick = st;
+  }
+  if (pick == nullptr && g_stage.size() >= kMaxStaging) {
+    for (Staging* st : g_stage)  // recycle an idle one of this device: wait for its copy
+      if (!st->busy && st->device == dev) {
+        pick = st;
+        break;
+      }
+    if (pick != nullptr) {
+      if (hipEventSynchronize(pick->done) != hipSuccess) return nullptr;
+      if (pick->cap < bytes) {
+        (void)hipHostFree(pick->host);
+        pick->host = nullptr;
+        pick->cap = 0;
+      }
+    }
+  }
+  if (pick == nullptr) {
+    pick = new Staging;
+    pick->device = dev;
+    if (hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {
+      delete pick;
+      return nullptr;
+    }
+    g_stage.push_back(pick);
+  }
+  if (pick->cap < bytes) {
+    size_t cap = 64u << 10;
+    while (cap < bytes) cap <<= 1;
+    if (hipHostMalloc(&pick->host, cap, hipHostMallocDefault) != hipSuccess) {
+      pick->host = nullptr;
+      pick->cap = 0;
+      return nullptr;
+    }
+    pick->cap = cap;
+  }
+  pick->busy = true;
+  return pick;
+}
+
+// `stream` = where a copy from the buffer was queued (nullptr-able), or
+// `queued` = false when nothing was.
+void stage_release(Staging* st, bool queued, hipStream_t stream) {
+  if (queued) (void)hipEventRecord(st->done, stream);
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  st->busy = false;
 }
 
 // Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
@@ -159,6 +234,14 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
 // needs no recovery queues no device work at all.
 constexpr size_t kCopyFirstBitmapBytes = 256u << 10;
 
+// Work-list tiles are taken (automatic tiling) when at most this fraction of
+// the stripes lost a data block: then stripe and class tiles would leave most
+// of their tiles idle (sparse: 2.2x faster at 1 stripe in 9, skewed: 1.0-3.1x
+// at 1 in 5; tools/tiling_ab.py --pattern, profiles/r02n).  When every stripe
+// lost blocks, the bitmap tilings are as fast or faster (list tiles -1..-5 %
+// against the better of them, profiles/r02n/tiling_uniform.json, r02o).
+constexpr uint64_t kListStripesNum = 3, kListStripesDen = 4;
+
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k, size_t m,
                       const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream) {
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
@@ -170,20 +253,54 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   if (copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
                                    stream) != hipSuccess)
     return XEC_DEVICE_ERROR;
-  int needs = 0;
-  uint64_t lost = 0;
-  st = xec_scan_bitmap(h_bitmap, S, k, m, &needs, &lost);
+  // Work list: as many u32 entries as fit in the 4-byte-aligned part of the
+  // caller's S*(k+m)-byte scratch, staged in pinned host memory by the scan.
+  const int tiling = g_decode_tiling.load(std::memory_order_relaxed);
+  const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
+  const uint64_t cap = bitmap_bytes > pad ? (bitmap_bytes - pad) / 4 : 0;
+  int dev = 0;
+  Staging* sg = nullptr;
+  if ((tiling == 0 || tiling == 3) && k <= kWorkItemMaxK && S <= kWorkItemMaxStripes && cap > 0 &&
+      hipGetDevice(&dev) == hipSuccess)
+    sg = stage_acquire(cap * 4, dev);
+  XecScan scan;
+  st = xec_scan_bitmap(h_bitmap, S, k, m, &scan,
+                       sg ? static_cast<uint32_t*>(sg->host) : nullptr, sg ? cap : 0);
+  const bool list = sg != nullptr && st == XEC_SUCCESS && scan.lost_data <= cap &&
+                    (tiling == 3 ||
+                     scan.stripes_lost * kListStripesDen <= (uint64_t)S * kListStripesNum);
+  if (!list && sg != nullptr) stage_release(sg, false, stream);
   if (st != XEC_SUCCESS) return st;  // nothing but the scratch copy was queued
-  if (!needs) return XEC_SUCCESS;
+  if (!scan.needs_recovery || scan.lost_data == 0) {  // nothing to rebuild
+    if (list) stage_release(sg, false, stream);
+    return XEC_SUCCESS;
+  }
+  if (list) {
+    // stream-ordered after any bitmap copy into the same scratch
+    uint8_t* d_items = d_bitmap + pad;
+    const bool copied = hipMemcpyAsync(d_items, sg->host, scan.lost_data * 4,
+                                       hipMemcpyHostToDevice, stream) == hipSuccess;
+    stage_release(sg, copied, stream);
+    if (!copied) return XEC_DEVICE_ERROR;
+    // one reduction per tile, as encode: encode's residency table
+    const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+    const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+    return xec::launch_decode(d_data, d_parity, d_items, g, ls, xec::kDecodeListTiles, stream,
+                              scan.lost_data) == hipSuccess
+               ? XEC_SUCCESS
+               : XEC_DEVICE_ERROR;
+  }
   if (!copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
                                     stream) != hipSuccess)
     return XEC_DEVICE_ERROR;
   // class tiles: one reduction per tile, so the encode's residency table
-  const bool cls = use_class_tiles(S, m, lost);
-  const xec::LaunchShape ls =
-      launch_shape(bs, cls ? auto_occupancy(k / m) : decode_auto_occupancy(k / m, lost, S));
+  const bool cls = use_class_tiles(S, m, scan.lost_data);
+  const xec::LaunchShape ls = launch_shape(
+      bs, cls ? auto_occupancy(k / m) : decode_auto_occupancy(k / m, scan.lost_data, S));
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
-  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, cls, stream) == hipSuccess
+  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls,
+                            cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
+                            stream) == hipSuccess
              ? XEC_SUCCESS
              : XEC_DEVICE_ERROR;
 }
@@ -208,7 +325,9 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   if (xec::launch_check(d_bitmap, g, d_status, stream) != hipSuccess) return XEC_DEVICE_ERROR;
   g.gate = d_status;
-  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls, cls, stream) == hipSuccess
+  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls,
+                            cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
+                            stream) == hipSuccess
              ? XEC_SUCCESS
              : XEC_DEVICE_ERROR;
 }
@@ -273,7 +392,7 @@ xec_status xec_set_occupancy(int waves_per_simd) {
 }
 
 xec_status xec_set_decode_tiling(int tiling) {
-  if (tiling < 0 || tiling > 2) return XEC_INVALID_SIZE;
+  if (tiling < 0 || tiling > 3) return XEC_INVALID_SIZE;
   g_decode_tiling.store(tiling, std::memory_order_relaxed);
   return XEC_SUCCESS;
 }

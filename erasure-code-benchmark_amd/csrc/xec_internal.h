@@ -8,7 +8,24 @@
 
 #include "xec.h"
 
-// xec_check_bitmap plus the number of lost (zero) data bytes in the batch;
-// lost_data may be null.  Defined in xec_scan.cpp.
-xec_status xec_scan_bitmap(const uint8_t* h_bitmap, size_t S, size_t k, size_t m,
-                           int* needs_recovery, uint64_t* lost_data);
+// One decode work item: a lost data block, stripe c, block i (i < k <= 256,
+// c < 2^24), packed as c << 8 | i (xec_kernels.hip decode_list_kernel).
+constexpr size_t kWorkItemMaxK = 256;
+constexpr size_t kWorkItemMaxStripes = size_t(1) << 24;
+inline uint32_t xec_work_item(size_t c, size_t i) {
+  return static_cast<uint32_t>(c << 8) | static_cast<uint32_t>(i);
+}
+
+// What one host pass over a batch bitmap finds (xec_scan_bitmap).
+struct XecScan {
+  int needs_recovery = 0;     // require_recovery over the batch (bit 0 of a data byte clear)
+  uint64_t lost_data = 0;     // zero data bytes
+  uint64_t stripes_lost = 0;  // stripes with at least one zero data byte
+};
+
+// xec_check_bitmap plus the counts above (out may be null) and, when `items`
+// is non-null, the first `cap` lost data blocks as work items in batch order
+// (requires k <= kWorkItemMaxK and S <= kWorkItemMaxStripes).  Defined in
+// xec_scan.cpp.
+xec_status xec_scan_bitmap(const uint8_t* h_bitmap, size_t S, size_t k, size_t m, XecScan* out,
+                           uint32_t* items, uint64_t cap);

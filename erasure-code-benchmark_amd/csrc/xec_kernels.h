@@ -54,11 +54,16 @@ inline uint32_t grid_for(uint64_t work_items, uint32_t max_grid, uint32_t thread
 
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
                          const LaunchShape& ls, hipStream_t s);
-// class_tiles: one tile per (stripe, class, chunk) -- for batches where
-// (nearly) every class lost a block; else one per (stripe, chunk).
+// Decode tilings.  Stripe: one tile per (stripe, chunk), d_bitmap = the batch
+// bitmap.  Class: one per (stripe, class, chunk), d_bitmap = the bitmap.
+// List: one per (work item, chunk), d_bitmap = n_items u32 work items
+// (xec_internal.h xec_work_item), 4-byte aligned.
+constexpr int kDecodeStripeTiles = 0;
+constexpr int kDecodeClassTiles = 1;
+constexpr int kDecodeListTiles = 2;
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
-                         const Geometry& g, const LaunchShape& ls, bool class_tiles,
-                         hipStream_t s);
+                         const Geometry& g, const LaunchShape& ls, int tiling, hipStream_t s,
+                         uint64_t n_items = 0);
 // Device-side recoverability check (xorec_utils.hpp:160-175 over the batch):
 // *d_status |= 4 if some class of some stripe lost two or more blocks.  The
 // caller zeroes *d_status first (stream-ordered).

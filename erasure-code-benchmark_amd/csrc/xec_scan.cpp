@@ -37,7 +37,11 @@ struct Visitor {
   size_t cur_stripe = 0, row_start = 0;
   int need = 0;
   uint64_t lost_data = 0;  // zero data bytes seen
+  uint64_t stripes_lost = 0;
+  size_t last_lost_stripe = ~size_t(0);
   std::vector<uint32_t> mark;  // stripe+1 that last marked each class
+  uint32_t* items = nullptr;   // optional work list (xec_scan_bitmap)
+  uint64_t cap = 0;
 
   Visitor(const uint8_t* b, size_t k_, size_t m_) : bm(b), k(k_), m(m_), row(k_ + m_), mark(m_, 0) {}
 
@@ -51,7 +55,14 @@ struct Visitor {
     const size_t i = pos - row_start;
     if (i < k) need = 1;
     if (v != 0) return true;  // bit 0 clear but nonzero: present for is_recoverable
-    if (i < k) ++lost_data;
+    if (i < k) {
+      if (lost_data < cap) items[lost_data] = xec_work_item(cur_stripe, i);
+      ++lost_data;
+      if (last_lost_stripe != cur_stripe) {
+        last_lost_stripe = cur_stripe;
+        ++stripes_lost;
+      }
+    }
     const size_t cls = i < k ? (m == 1 ? 0 : i % m) : i - k;
     const uint32_t tag = static_cast<uint32_t>(cur_stripe) + 1u;
     if (mark[cls] == tag) return false;
@@ -114,8 +125,8 @@ bool scan_range(Visitor& v, size_t n) {
 // which checks classes with a bit set.  ~1.5 ns per stripe against ~5 ns for
 // the per-candidate visitor, whose stripe bookkeeping mispredicts.
 __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm, size_t S,
-                                                             size_t k, size_t m, int* need_out,
-                                                             uint64_t* lost_out) {
+                                                             size_t k, size_t m, XecScan* out,
+                                                             uint32_t* items, uint64_t cap) {
   const size_t row = k + m;
   const uint64_t row_mask = row == 64 ? ~0ull : ((1ull << row) - 1);
   const uint64_t data_mask = (1ull << k) - 1;  // k < row <= 64
@@ -124,7 +135,7 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
   const __m256i one = _mm256_set1_epi8(1), zero = _mm256_setzero_si256();
   const size_t n = S * row;
   alignas(32) uint8_t pad[64];
-  uint64_t need = 0, lost = 0;
+  uint64_t need = 0, lost = 0, stripes_lost = 0;
   for (size_t c = 0; c < S; ++c) {
     const uint8_t* r = bm + c * row;
     if (c * row + 64 > n) {  // last rows: never read past the caller's buffer
@@ -143,7 +154,14 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
          static_cast<uint64_t>(static_cast<uint32_t>(
              _mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_and_si256(x1, one), zero)))) << 32);
     need |= e & data_mask;
-    lost += static_cast<uint64_t>(__builtin_popcountll(z & data_mask));
+    uint64_t zd = z & data_mask;
+    if (items != nullptr) {  // lost data blocks, in order (rare: most rows have none)
+      for (uint64_t q = lost; zd; zd &= zd - 1, ++q)
+        if (q < cap) items[q] = xec_work_item(c, static_cast<size_t>(__builtin_ctzll(zd)));
+      zd = z & data_mask;
+    }
+    lost += static_cast<uint64_t>(__builtin_popcountll(zd));
+    stripes_lost += zd != 0;
     if (z & (z - 1)) {  // two or more zero bytes: they must be in different classes
       if (m == 1) return 0;
       uint64_t seen = 0, bits = z;
@@ -155,41 +173,49 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
       }
     }
   }
-  *need_out = need != 0;
-  *lost_out = lost;
+  out->needs_recovery = need != 0;
+  out->lost_data = lost;
+  out->stripes_lost = stripes_lost;
   return 1;
 }
 #endif
 
 }  // namespace
 
-// Also counts the zero (lost) data bytes of the batch: xec_decode sizes the
-// decode launch's residency by the rebuild work per stripe.
-xec_status xec_scan_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m, int* needs,
-                           uint64_t* lost_data) {
-  if (needs) *needs = 0;
-  if (lost_data) *lost_data = 0;
+// Also counts the zero (lost) data bytes and the stripes that have one and,
+// when `items` is given, lists the first `cap` of them in batch order
+// (xec_work_item).
+xec_status xec_scan_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m, XecScan* out,
+                           uint32_t* items, uint64_t cap) {
+  XecScan r;
+  if (out) *out = r;
   if (k < 1 || m < 1 || k % m != 0) return XEC_INVALID_COUNTS;
 #if defined(__x86_64__)
   static const bool fast = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi") &&
                            __builtin_cpu_supports("popcnt");
   if (fast && k + m <= 64 && m <= 64 && S > 0) {
-    int need = 0;
-    uint64_t lost = 0;
-    if (!scan_rows_avx2(bm, S, k, m, &need, &lost)) return XEC_DECODE_FAILURE;
-    if (needs) *needs = need;
-    if (lost_data) *lost_data = lost;
+    if (!scan_rows_avx2(bm, S, k, m, &r, items, cap)) return XEC_DECODE_FAILURE;
+    if (out) *out = r;
     return XEC_SUCCESS;
   }
 #endif
   Visitor v(bm, k, m);
+  if (items != nullptr) {
+    v.items = items;
+    v.cap = cap;
+  }
   if (!scan_range(v, S * (k + m))) return XEC_DECODE_FAILURE;
-  if (needs) *needs = v.need;
-  if (lost_data) *lost_data = v.lost_data;
+  r.needs_recovery = v.need;
+  r.lost_data = v.lost_data;
+  r.stripes_lost = v.stripes_lost;
+  if (out) *out = r;
   return XEC_SUCCESS;
 }
 
 extern "C" xec_status xec_check_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m,
                                        int* needs) {
-  return xec_scan_bitmap(bm, S, k, m, needs, nullptr);
+  XecScan r;
+  const xec_status st = xec_scan_bitmap(bm, S, k, m, &r, nullptr, 0);
+  if (needs) *needs = r.needs_recovery;
+  return st;
 }

@@ -106,7 +106,7 @@ def set_occupancy(waves_per_simd: int = 0) -> Status:
 
 def set_decode_tiling(tiling: int = 0) -> Status:
     """xec_set_decode_tiling; 0 = automatic (default), 1 = stripe tiles, 2 = class tiles
-    (m > 1 only; identical results)."""
+    (m > 1 only), 3 = work-list tiles where the list fits (identical results)."""
     return Status(lib().xec_set_decode_tiling(tiling))
 
 

@@ -69,17 +69,23 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * Host checks follow the reference: XEC_DECODE_FAILURE if ANY stripe is
  * unrecoverable (is_recoverable, xorec_utils.hpp:160-175) and then no data is
  * touched; XEC_SUCCESS without a kernel if no stripe needs recovery
- * (require_recovery, xorec_utils.hpp:144-149).  Otherwise h_bitmap is copied
- * to d_bitmap on `stream` and every lost data block is rebuilt:
+ * (require_recovery, xorec_utils.hpp:144-149).  Otherwise every lost data
+ * block is rebuilt:
  *   data[c][i] = parity[c][i%m] ^ XOR_{l%m == i%m, l != i} data[c][l].
+ * d_bitmap is scratch for the call: it receives on `stream` a copy of
+ * h_bitmap and/or the list of lost data blocks the host scan found (4 bytes
+ * each; used when at most 3/4 of the stripes lost a data block and the list
+ * fits in its S*(k+m) bytes, k <= 256, S <= 2^24: one tile per lost block and
+ * 1 KiB chunk, xec_set_decode_tiling).
  * Lost parity is not regenerated.  Parity is READ-ONLY here, as in the CPU
  * decode (xorec.cpp:62-111) -- deliberately unlike the reference GPU decode,
  * which folds all data into parity (xorec_gpu_cmp.cu:94-102).  The content of
  * lost data blocks on entry is irrelevant (no zeroing pre-condition).
- * For bitmaps of 256 KiB and more (S*(k+m) bytes) the copy into d_bitmap is
- * queued before the host scan, so the two overlap; d_bitmap is then written
- * whatever the verdict (it is scratch).  h_bitmap must stay unchanged until
- * the stream has passed the call, as for any asynchronous copy. */
+ * The list is staged in pinned host memory the library keeps for reuse (the
+ * only memory it holds across calls).  Bitmaps of 256 KiB and more are copied
+ * before the host scan so the two overlap, and d_bitmap is then written
+ * whatever the verdict.  h_bitmap must stay unchanged until the stream has
+ * passed the call, as for any asynchronous copy. */
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                       size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream);
 
@@ -158,16 +164,19 @@ xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_
  * 0..8. */
 xec_status xec_set_occupancy(int waves_per_simd);
 
-/* Tuning / diagnostics (no reference counterpart): how decode tiles the
- * batch when m > 1.  0 = automatic (default): xec_decode counts the lost data
- * blocks in its host scan and uses class tiles -- one tile per (stripe,
- * class, 1 KiB column chunk), one class reduction each, encode's tiling --
+/* Tuning / diagnostics (no reference counterpart): how xec_decode tiles the
+ * batch.  0 = automatic (default): work-list tiles -- one per (lost data
+ * block, 1 KiB column chunk), from the list the host scan builds -- when at
+ * most 3/4 of the stripes lost a data block and the list fits the scratch
+ * (see xec_decode); otherwise class tiles -- one
+ * per (stripe, class, chunk), one class reduction each, encode's tiling --
  * when the batch lost more than one data block per stripe on average and at
- * least half of its S*m classes lost one, else stripe
- * tiles -- one per (stripe, chunk), rebuilding the stripe's lost blocks one
- * after another; xec_decode_device (no host scan) uses stripe tiles.
- * 1 = always stripe tiles, 2 = always class tiles.  Results are identical;
- * only the speed differs.  XEC_INVALID_SIZE outside 0..2. */
+ * least half of its S*m classes lost one, else stripe tiles -- one per
+ * (stripe, chunk), rebuilding the stripe's lost blocks one after another.
+ * xec_decode_device (no host scan) uses stripe tiles.  1 = always stripe
+ * tiles, 2 = always class tiles, 3 = work-list tiles where the list fits (else
+ * the automatic bitmap choice).  Results are identical; only the speed
+ * differs.  XEC_INVALID_SIZE outside 0..3. */
 xec_status xec_set_decode_tiling(int tiling);
 
 /* Tuning / diagnostics (no reference counterpart): kernel shape of

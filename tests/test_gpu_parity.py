@@ -227,10 +227,13 @@ def test_encode_is_linear(gpu):
     assert torch.equal(torch.bitwise_xor(a.p, bb.p), pab)
 
 
-@pytest.mark.parametrize("tiling", [0, 1, 2])
+@pytest.mark.parametrize("tiling", [0, 1, 2, 3])
 @pytest.mark.parametrize("S,k,m,bs,pattern", [
-    (64, 16, 2, 65536, "all"),      # every class lost a data block: class tiles (auto)
-    (48, 16, 8, 8192, "all"),
+    (64, 16, 2, 65536, "all"),      # every class lost a data block
+    (48, 16, 8, 8192, "all"),       # 8 per stripe > the 6 list entries the scratch holds: bitmap
+    (64, 16, 4, 4096, "sparse"),    # a few stripes lost a block, most none
+    (64, 16, 8, 2048, "skew"),      # some stripes lost a block in every class, the rest none
+    (3, 264, 8, 256, "all"),        # k > 256: no work list, bitmap path
     (40, 32, 8, 4352, "all"),       # ragged tail tile
     (33, 8, 2, 2048, "all"),
     (50, 16, 4, 4096, "half"),      # half the classes: class tiles with idle tiles (auto)
@@ -241,8 +244,9 @@ def test_encode_is_linear(gpu):
     (7, 15, 5, 512, "all"),         # generic member count 3
 ])
 def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
-    """xec_set_decode_tiling: stripe tiles, class tiles and the automatic choice
-    rebuild the same bytes, whatever fraction of the classes lost a block."""
+    """xec_set_decode_tiling: stripe tiles, class tiles, work-list tiles and the
+    automatic choice rebuild the same bytes, whatever fraction of the classes
+    lost a block and however the losses spread over the stripes."""
     b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
     bm = np.ones((S, k + m), np.uint8)
     rng = np.random.default_rng(S * 1000 + k)
@@ -255,6 +259,13 @@ def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
                 bm[c, j + m * int(rng.integers(k // m))] = 0
         elif pattern == "one":
             bm[c, int(rng.integers(k))] = 0
+        elif pattern == "sparse":
+            if c % 9 == 4:
+                bm[c, int(rng.integers(k))] = 0
+        elif pattern == "skew":
+            if c % 5 == 0:
+                for j in range(m):
+                    bm[c, j + m * int(rng.integers(k // m))] = 0
         elif pattern == "parity":
             lost_par = int(rng.integers(m))
             bm[c, k + lost_par] = 0
@@ -270,7 +281,7 @@ def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
         gpu.set_decode_tiling(0)
 
 
-@pytest.mark.parametrize("tiling", [1, 2])
+@pytest.mark.parametrize("tiling", [1, 2, 3])
 def test_golden_decode_fixtures_each_tiling(gpu, oracle, known_answers, tiling):
     assert gpu.set_decode_tiling(tiling) == gpu.Status.SUCCESS
     try:
@@ -280,7 +291,7 @@ def test_golden_decode_fixtures_each_tiling(gpu, oracle, known_answers, tiling):
 
 
 def test_decode_tiling_argument_range(gpu):
-    assert gpu.set_decode_tiling(3) == gpu.Status.INVALID_SIZE
+    assert gpu.set_decode_tiling(4) == gpu.Status.INVALID_SIZE
     assert gpu.set_decode_tiling(-1) == gpu.Status.INVALID_SIZE
     assert gpu.set_decode_tiling(0) == gpu.Status.SUCCESS
 

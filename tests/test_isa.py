@@ -25,7 +25,7 @@ def kernels() -> dict[str, dict]:
     subprocess.run(["make", "-C", str(PKG_DIR), "asm"], check=True, capture_output=True)
     text = ASM.read_text()
     out = {}
-    for m in re.finditer(r"^(_ZN3xec1[0-9](encode|decode)_kernel\w+):.*?^\s*s_endpgm", text,
+    for m in re.finditer(r"^(_ZN3xec1[0-9](encode|decode)_(?:class_|list_)?kernel\w+):.*?^\s*s_endpgm", text,
                          re.S | re.M):
         out[m.group(1)] = {"body": m.group(0)}
     meta = re.findall(r"\.name:\s+(\S+)\n(.*?)\.vgpr_count:\s+(\d+)", text, re.S)
@@ -54,10 +54,10 @@ def test_nt_kernels_carry_their_cache_policy(kernels):
         assert loads and stores, name
         missing = [i for i in loads if not re.search(r"\bnt\b", i)]
         assert not missing, f"{name}: {missing[:3]}"
-        want = r"\bsc1\b" if "decode_kernel" in name else r"\bnt\b"
+        want = r"\bsc1\b" if "decode_" in name else r"\bnt\b"
         wrong = [i for i in stores if not re.search(want, i)]
         assert not wrong, f"{name}: {wrong[:3]}"
-        if "decode_kernel" in name:
+        if "decode_" in name:
             assert not [i for i in stores if re.search(r"\bnt\b", i)], name
 
 
@@ -66,7 +66,7 @@ def test_nt_kernels_carry_their_cache_policy(kernels):
 AUTO_OCCUPANCY = {4: 4, 8: 4, 16: 2, 32: 1}
 
 
-@pytest.mark.parametrize("kind", ["encode", "decode"])
+@pytest.mark.parametrize("kind", ["encode", "decode", "decode_class", "decode_list"])
 @pytest.mark.parametrize("nm", sorted(AUTO_OCCUPANCY))
 def test_registers_admit_the_default_residency(kernels, kind, nm):
     hits = [k for n, k in kernels.items()

@@ -2,14 +2,18 @@
 """In-process A/B of the decode tilings (xec_set_decode_tiling) on one MI355X.
 
 For each shape and each number of lost data blocks per stripe (one per class,
-bench.erasure_pattern), times xec_decode with stripe tiles (1), class tiles (2)
-and the automatic choice (0) in interleaved rounds on the same buffers (three
+bench.erasure_pattern), times xec_decode with stripe tiles (1), class tiles (2),
+work-list tiles (3) and the automatic choice (0) in interleaved rounds on the
+same buffers (three
 rotating buffer sets, HIP events on the launching stream), and checks every
 variant rebuilt the erased blocks bit-exactly (against a fresh device fill).
 Also times encode on the same buffers as the reference point.  Rates are
-algorithmic GB/s: decode S*lost*(k/m+1)*bs, encode S*(k+m)*bs per launch.
+algorithmic GB/s: decode (lost data blocks)*(k/m+1)*bs, encode S*(k+m)*bs per
+launch.  --pattern sparse keeps the losses of only every 9th stripe, skew only
+every 5th (the others lose nothing).
 
-    python tools/tiling_ab.py [--shapes 16,2,1048576,256:16,8,65536,16384] [--out f.json]
+    python tools/tiling_ab.py [--shapes 16,2,1048576,256:16,8,65536,16384]
+                              [--pattern uniform|sparse|skew] [--out f.json]
 """
 from __future__ import annotations
 
@@ -39,6 +43,8 @@ def main():
                          "tiles at (variants class@oN); default: automatic residency only")
     ap.add_argument("--only-class", action="store_true",
                     help="time class tiles (and their --occ variants) and encode only")
+    ap.add_argument("--pattern", default="uniform", choices=["uniform", "sparse", "skew"])
+    ap.add_argument("--variants", default="", help="comma list to keep (e.g. class,list)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -62,21 +68,29 @@ def main():
             assert xec.fill_splitmix64(d, S, k * bs, 1000 + s * 7919, stream) == 0
             assert xec.encode(d, p, S, bs, k, m, stream) == 0
             sets.append((d, p))
-        b_enc, b_dec1 = algorithmic_bytes(S, k, m, bs)
+        b_enc, _ = algorithmic_bytes(S, k, m, bs)
         for lost in losts:
             if lost > m:
                 continue
             bm = erasure_pattern(np, S, k, m, lost)
+            if args.pattern != "uniform":
+                keep = np.arange(S) % (9 if args.pattern == "sparse" else 5) == 0
+                bm[~keep] = 1
+            lost_blocks = int((bm[:, :k] == 0).sum())
             h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
             d_bm = h_bm.to("cuda")
             scratch = [torch.empty_like(d_bm) for _ in range(3)]
             # variant -> (tiling, occupancy); occupancy None = automatic
-            variants = ({"stripe": (1, None), "class": (2, None), "auto": (0, None)} if m > 1
-                        else {"stripe": (1, None)})
+            variants = ({"stripe": (1, None), "class": (2, None), "list": (3, None),
+                         "auto": (0, None)} if m > 1
+                        else {"stripe": (1, None), "list": (3, None)})
             if args.only_class and m > 1:
                 variants = {"class": (2, None)}
             for o in (int(x) for x in args.occ.split(",") if x):
                 variants[f"class@o{o}"] = (2 if m > 1 else 1, o)
+            if args.variants:
+                keep = set(args.variants.split(","))
+                variants = {v: t for v, t in variants.items() if v in keep}
             times = {v: [] for v in variants}
             times["encode"] = []
             it = 0
@@ -114,8 +128,9 @@ def main():
             assert xec.set_decode_tiling(0) == 0
             assert xec.set_occupancy(0) == 0
             del fresh
-            b_dec = b_dec1 * lost
-            row = {"k": k, "m": m, "bs": bs, "S": S, "lost_per_stripe": lost,
+            b_dec = lost_blocks * (k // m + 1) * bs
+            row = {"k": k, "m": m, "bs": bs, "S": S, "pattern": args.pattern,
+                   "lost_per_stripe": lost, "lost_blocks": lost_blocks,
                    "class_fraction": lost / m, "bit_exact": ok}
             for v, ts in times.items():
                 med = statistics.median(ts)
