@@ -53,13 +53,18 @@ uint32_t lds_for_occupancy(int waves, int threads) {
 // 16, hipcc's rolling window; all 32 at k/m = 32); the best residency keeps
 // roughly 16-32 KiB in flight per SIMD -- 8 waves per SIMD at k/m = 16 queue
 // 4x the requests and ran 3 % (encode) to 6 % (decode) slower.  0 = no cap
-// (8 per SIMD).
+// (8 per SIMD).  Member counts without a compiled unroll run the generic loop
+// (8 loads in flight per group); swept at 3, 5, 6, 12, 24, 48 and 64
+// (profiles/r02q): no cap below 8 members, 4 waves from 8 (12: +6 / +5 %
+// encode / decode), 2 from 20 (24: +8 / +8 %, 48: +4 / +7 %), 1 from 56
+// (64: +6 / +3 %).
 int auto_occupancy(uint64_t nm) {
   switch (nm) {
+    case 1: case 2: return 0;
     case 4: case 8: return 4;
     case 16: return 2;
     case 32: return 1;
-    default: return 0;
+    default: return nm < 8 ? 0 : nm < 20 ? 4 : nm < 56 ? 2 : 1;
   }
 }
 

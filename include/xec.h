@@ -158,8 +158,9 @@ xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_
  * at most `waves_per_simd` (1..8; 8 = no cap) waves resident per SIMD,
  * enforced by reserving LDS per workgroup (the kernels use none).
  * 0 = automatic (the default): the cap measured fastest for the member count
- * k/m at the default launch shape -- 1 at k/m = 32, 2 at 16, 4 at 4 and 8,
- * none otherwise.  The reserved LDS keeps other kernels' LDS
+ * k/m at the default launch shape -- 1 at k/m = 32, 2 at 16, 4 at 4 and 8;
+ * for other member counts none below 8, 4 below 20, 2 below 56, else 1;
+ * none at 1 and 2.  The reserved LDS keeps other kernels' LDS
  * users off those CUs while a launch runs.  Returns XEC_INVALID_SIZE outside
  * 0..8. */
 xec_status xec_set_occupancy(int waves_per_simd);
