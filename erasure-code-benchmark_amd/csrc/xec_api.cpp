@@ -167,9 +167,12 @@ Staging* stage_acquire(size_t bytes, int dev) {
 }
 
 // `stream` = where a copy from the buffer was queued (nullptr-able), or
-// `queued` = false when nothing was.
+// `queued` = false when nothing was.  If the event cannot be recorded there
+// (a stream of another device than the one current when the buffer was
+// made), the copy is waited for instead, so the buffer is never reused early.
 void stage_release(Staging* st, bool queued, hipStream_t stream) {
-  if (queued) (void)hipEventRecord(st->done, stream);
+  if (queued && hipEventRecord(st->done, stream) != hipSuccess)
+    (void)hipStreamSynchronize(stream);
   std::lock_guard<std::mutex> lk(g_stage_mu);
   st->busy = false;
 }
