@@ -42,6 +42,8 @@ def main():
                     help="comma list of xec_set_occupancy values to cross with --libs "
                          "(0 = automatic, 8 = none); default: each lib's default only")
     ap.add_argument("--lost", type=int, default=1, help="lost data blocks per stripe (1..m)")
+    ap.add_argument("--tiling", type=int, default=0,
+                    help="xec_set_decode_tiling for every lib (0 = automatic)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -53,6 +55,8 @@ def main():
     torch.cuda.set_device(0)
     assert xec.init(0) == 0
     loaded = {n: load(n) for n in args.libs.split(",")}
+    for L in loaded.values():
+        assert L.xec_set_decode_tiling(args.tiling) == 0
     occs = [int(x) for x in args.occ.split(",")] if args.occ else [None]
     libs = {}
     for n, L in loaded.items():
