@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--decode-api", default="host", choices=["host", "device"],
                     help="host: xec_decode (reference-shaped: host bitmap scan + H2D copy); "
                          "device: xec_decode_device (bitmap resident, verdict on the device)")
+    ap.add_argument("--decode-tiling", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="xec_set_decode_tiling (diagnostic; 0 = the library's automatic choice)")
     ap.add_argument("--dist-world1", action="store_true",
                     help="at N=1, still open a one-rank process group (RCCL with nccl) and run "
                          "the collectives and the scatter/gather leg: exercises the N>1 "
@@ -401,6 +403,8 @@ def run_rank(args):
     st = xec.init(dev)
     if st != 0:
         sys.exit(f"xec_init({dev}) failed: {st!r}")
+    if args.decode_tiling and xec.set_decode_tiling(args.decode_tiling) != 0:
+        sys.exit(f"--decode-tiling {args.decode_tiling} rejected")
     use_dist = world > 1 or args.dist_world1
     if use_dist:
         if backend == "nccl":
@@ -538,6 +542,13 @@ def run_rank(args):
             ok &= bool(torch.equal(fresh, d))
         del fresh
 
+    # which decode kernel xec_decode's tiling launched (xec_decode_tiling_used)
+    if args.decode_api == "device":
+        dec_kernel = "xec::decode_kernel (xec_decode_device)"
+    elif hasattr(xec, "decode_tiling_used"):
+        dec_kernel = xec.DECODE_KERNELS.get(xec.decode_tiling_used(), "xec::decode_kernel")
+    else:  # CPU rehearsal stand-ins
+        dec_kernel = "xec::decode_kernel"
     # every rank's (elapsed, encode ms, decode ms, failed, stripes); rank 0 reports
     # the max time over ranks and each rank's own rates
     # which device this rank ran on (PCI bus id), so the line shows N distinct GPUs
@@ -584,7 +595,7 @@ def run_rank(args):
         # the dominant kernel is the one the step spends longer in (decode at the
         # BASELINE shapes: in-place writes); both are reported
         rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic),
-              "decode": roofline("xec::decode_kernel", b_dec, dec_ms, traffic_dec)}
+              "decode": roofline(dec_kernel, b_dec, dec_ms, traffic_dec)}
         dominant = "decode" if dec_ms >= enc_ms else "encode"
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.lost == 1 and not args.rehearse_cpu:
@@ -613,7 +624,8 @@ def run_rank(args):
                        "parallelism": f"stripe-partition x{world} (no data-path collective)",
                        "bytes_convention": "algorithmic: enc S(k+m)bs + dec S(k/m+1)bs",
                        "decode_api": "xec_decode_device" if args.decode_api == "device"
-                       else "xec_decode"},
+                       else "xec_decode",
+                       "decode_tiling": args.decode_tiling or "automatic"},
             "roofline": dict(rl[dominant], dominant_by="avg launch time"),
             "roofline_by_kernel": rl,
             "cpu_baseline": cpu,

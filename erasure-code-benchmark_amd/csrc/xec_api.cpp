@@ -29,6 +29,7 @@ std::atomic<int> g_nt{0};
 std::atomic<int> g_threads{0};
 std::atomic<int> g_occupancy{0};  // xec_set_occupancy: waves per SIMD, 0 = automatic
 std::atomic<int> g_decode_tiling{0};  // xec_set_decode_tiling: 0 auto, 1 stripe, 2 class, 3 list
+thread_local int g_tiling_used = 0;   // xec_decode_tiling_used: this thread's last xec_decode
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
@@ -252,6 +253,7 @@ constexpr uint64_t kListStripesNum = 3, kListStripesDen = 4;
 
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k, size_t m,
                       const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream) {
+  g_tiling_used = 0;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
@@ -261,57 +263,80 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   if (copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
                                    stream) != hipSuccess)
     return XEC_DEVICE_ERROR;
-  // Work list: as many u32 entries as fit in the 4-byte-aligned part of the
-  // caller's S*(k+m)-byte scratch, staged in pinned host memory by the scan.
-  const int tiling = g_decode_tiling.load(std::memory_order_relaxed);
-  const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
-  const uint64_t cap = bitmap_bytes > pad ? (bitmap_bytes - pad) / 4 : 0;
-  int dev = 0;
-  Staging* sg = nullptr;
-  if ((tiling == 0 || tiling == 3) && k <= kWorkItemMaxK && S <= kWorkItemMaxStripes && cap > 0 &&
-      hipGetDevice(&dev) == hipSuccess)
-    sg = stage_acquire(cap * 4, dev);
   XecScan scan;
-  st = xec_scan_bitmap(h_bitmap, S, k, m, &scan,
-                       sg ? static_cast<uint32_t*>(sg->host) : nullptr, sg ? cap : 0);
-  const bool list = sg != nullptr && st == XEC_SUCCESS && scan.lost_data <= cap &&
-                    (tiling == 3 ||
-                     scan.stripes_lost * kListStripesDen <= (uint64_t)S * kListStripesNum);
-  if (!list && sg != nullptr) stage_release(sg, false, stream);
+  st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
   if (st != XEC_SUCCESS) return st;  // nothing but the scratch copy was queued
-  if (!scan.needs_recovery || scan.lost_data == 0) {  // nothing to rebuild
-    if (list) stage_release(sg, false, stream);
-    return XEC_SUCCESS;
-  }
-  if (list) {
-    // stream-ordered after any bitmap copy into the same scratch
-    uint8_t* d_items = d_bitmap + pad;
-    const bool copied = hipMemcpyAsync(d_items, sg->host, scan.lost_data * 4,
-                                       hipMemcpyHostToDevice, stream) == hipSuccess;
-    stage_release(sg, copied, stream);
-    if (!copied) return XEC_DEVICE_ERROR;
+  if (!scan.needs_recovery || scan.lost_data == 0) return XEC_SUCCESS;  // nothing to rebuild
+  // Which tiling: list tiles when the losses are sparse (or forced); for a
+  // list short enough to travel in the kernel arguments also wherever stripe
+  // tiles would run (no copy at all); class tiles keep dense multi-erasure
+  // batches.  The list is built by a second, listing pass only
+  // when it is used (the first pass costs ~1.1 ns per stripe).
+  const int tiling = g_decode_tiling.load(std::memory_order_relaxed);
+  const bool listable =
+      (tiling == 0 || tiling == 3) && k <= kWorkItemMaxK && S <= kWorkItemMaxStripes;
+  const bool small = scan.lost_data <= xec::kArgItems;
+  const bool sparse = scan.stripes_lost * kListStripesDen <= (uint64_t)S * kListStripesNum;
+  const bool cls = use_class_tiles(S, m, scan.lost_data);
+  if (listable && (tiling == 3 || sparse || (!cls && small))) {
     // one reduction per tile, as encode: encode's residency table
     const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
     const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
-    return xec::launch_decode(d_data, d_parity, d_items, g, ls, xec::kDecodeListTiles, stream,
-                              scan.lost_data) == hipSuccess
-               ? XEC_SUCCESS
-               : XEC_DEVICE_ERROR;
+    if (small) {  // the launch copies the list into its kernel arguments
+      uint32_t items[xec::kArgItems];
+      st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, items, xec::kArgItems);
+      if (st != XEC_SUCCESS) return st;
+      g_tiling_used = XEC_TILING_ARG_LIST;
+      return xec::launch_decode(d_data, d_parity, nullptr, g, ls, xec::kDecodeArgListTiles,
+                                stream, scan.lost_data, items) == hipSuccess
+                 ? XEC_SUCCESS
+                 : XEC_DEVICE_ERROR;
+    }
+    // Device list: u32 entries in the 4-byte-aligned part of the caller's
+    // S*(k+m)-byte scratch, staged in pinned host memory by the listing pass.
+    const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
+    const uint64_t cap = bitmap_bytes > pad ? (bitmap_bytes - pad) / 4 : 0;
+    int dev = 0;
+    Staging* sg = nullptr;
+    if (scan.lost_data <= cap && hipGetDevice(&dev) == hipSuccess)
+      sg = stage_acquire(scan.lost_data * 4, dev);
+    if (sg != nullptr) {
+      st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, static_cast<uint32_t*>(sg->host),
+                           scan.lost_data);
+      if (st != XEC_SUCCESS) {
+        stage_release(sg, false, stream);
+        return st;
+      }
+      // stream-ordered after any bitmap copy into the same scratch
+      uint8_t* d_items = d_bitmap + pad;
+      const bool copied = hipMemcpyAsync(d_items, sg->host, scan.lost_data * 4,
+                                         hipMemcpyHostToDevice, stream) == hipSuccess;
+      stage_release(sg, copied, stream);
+      if (!copied) return XEC_DEVICE_ERROR;
+      g_tiling_used = XEC_TILING_LIST;
+      return xec::launch_decode(d_data, d_parity, d_items, g, ls, xec::kDecodeListTiles, stream,
+                                scan.lost_data) == hipSuccess
+                 ? XEC_SUCCESS
+                 : XEC_DEVICE_ERROR;
+    }
+    // denser than the scratch holds as a list (or no staging memory): bitmap
   }
   if (!copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
                                     stream) != hipSuccess)
     return XEC_DEVICE_ERROR;
   // class tiles: one reduction per tile, so the encode's residency table
-  const bool cls = use_class_tiles(S, m, scan.lost_data);
   const xec::LaunchShape ls = launch_shape(
       bs, cls ? auto_occupancy(k / m) : decode_auto_occupancy(k / m, scan.lost_data, S));
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+  g_tiling_used = cls && m > 1 ? XEC_TILING_CLASS : XEC_TILING_STRIPE;
   return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls,
                             cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
                             stream) == hipSuccess
              ? XEC_SUCCESS
              : XEC_DEVICE_ERROR;
 }
+
+int xec_decode_tiling_used(void) { return g_tiling_used; }
 
 xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                              size_t m, const uint8_t* d_bitmap, int32_t* d_status,

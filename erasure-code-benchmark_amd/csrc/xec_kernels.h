@@ -58,12 +58,19 @@ hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
 // bitmap.  Class: one per (stripe, class, chunk), d_bitmap = the bitmap.
 // List: one per (work item, chunk), d_bitmap = n_items u32 work items
 // (xec_internal.h xec_work_item), 4-byte aligned.
+// ArgList: list tiles over up to kArgItems work items passed by value in the
+// kernel arguments (h_items, host memory, read at launch): no copy at all.
 constexpr int kDecodeStripeTiles = 0;
 constexpr int kDecodeClassTiles = 1;
 constexpr int kDecodeListTiles = 2;
+constexpr int kDecodeArgListTiles = 3;
+constexpr uint64_t kArgItems = 1024;
+struct ArgItems {
+  uint32_t v[kArgItems];
+};
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
                          const Geometry& g, const LaunchShape& ls, int tiling, hipStream_t s,
-                         uint64_t n_items = 0);
+                         uint64_t n_items = 0, const uint32_t* h_items = nullptr);
 // Device-side recoverability check (xorec_utils.hpp:160-175 over the batch):
 // *d_status |= 4 if some class of some stripe lost two or more blocks.  The
 // caller zeroes *d_status first (stream-ordered).

@@ -26,6 +26,7 @@
 // indices of xorec_gpu_cmp.cu:127-131).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstring>
 
 #include "xec_kernels.h"
 
@@ -279,24 +280,44 @@ __global__ __launch_bounds__(T) void decode_class_kernel(uint8_t* data,
 // Tile t reads its entry with one scalar load.
 // ---------------------------------------------------------------------------
 template <int NM, int U, bool NT, int T>
+__device__ __forceinline__ void rebuild_item(uint8_t* data, const uint8_t* __restrict__ parity,
+                                             uint32_t item, uint64_t chunk, const Geometry& g) {
+  const uint32_t nm = NM > 0 ? (uint32_t)NM : (uint32_t)g.nm;
+  const uint32_t m = (uint32_t)g.m;
+  const uint64_t stride = g.m * g.bs;
+  const uint64_t c = item >> 8;
+  const uint32_t i = item & 0xFFu;
+  const uint32_t j = i % m, r = i / m;  // class and member of the lost block
+  uint8_t* base = data + (c * g.k + j) * g.bs;
+  const uint64_t off = (chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+  xor_members<NM, U, NT, T, kDecodeStoreAux>(base, stride, parity + (c * g.m + j) * g.bs, (int)r,
+                                             base + (uint64_t)r * stride, off, g.bs, nm);
+}
+
+template <int NM, int U, bool NT, int T>
 __global__ __launch_bounds__(T) void decode_list_kernel(uint8_t* data,
                                                         const uint8_t* __restrict__ parity,
                                                         const uint32_t* __restrict__ items,
                                                         Geometry g) {
-  const uint32_t nm = NM > 0 ? (uint32_t)NM : (uint32_t)g.nm;
-  const uint32_t m = (uint32_t)g.m;
-  const uint64_t stride = g.m * g.bs;
   for (uint64_t t0 = blockIdx.x; t0 < g.total_tiles; t0 += gridDim.x) {
     const uint64_t t = g.total_tiles - 1 - t0;  // from the end of the batch, as encode
-    const uint64_t chunk = t % g.tiles_per_block;
     const uint32_t item = *(const_u32_as4)(items + t / g.tiles_per_block);
-    const uint64_t c = item >> 8;
-    const uint32_t i = item & 0xFFu;
-    const uint32_t j = i % m, r = i / m;  // class and member of the lost block
-    uint8_t* base = data + (c * g.k + j) * g.bs;
-    const uint64_t off = (chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
-    xor_members<NM, U, NT, T, kDecodeStoreAux>(base, stride, parity + (c * g.m + j) * g.bs,
-                                               (int)r, base + (uint64_t)r * stride, off, g.bs, nm);
+    rebuild_item<NM, U, NT, T>(data, parity, item, t % g.tiles_per_block, g);
+  }
+}
+
+// The same with the list in the kernel arguments (at most kArgItems entries;
+// the item is a scalar load from the kernarg segment): small decodes then
+// copy nothing to the device (a <= 8 KiB H2D copy runs as a blit kernel of its
+// own, 3.7-4.4 us, profiles/r02o, r02l).
+template <int NM, int U, bool NT, int T>
+__global__ __launch_bounds__(T) void decode_arglist_kernel(uint8_t* data,
+                                                           const uint8_t* __restrict__ parity,
+                                                           Geometry g, ArgItems items) {
+  for (uint64_t t0 = blockIdx.x; t0 < g.total_tiles; t0 += gridDim.x) {
+    const uint64_t t = g.total_tiles - 1 - t0;
+    rebuild_item<NM, U, NT, T>(data, parity, items.v[t / g.tiles_per_block],
+                               t % g.tiles_per_block, g);
   }
 }
 
@@ -370,8 +391,12 @@ hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t g
 
 template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
-                           int tiling, uint32_t grid, uint32_t lds, hipStream_t s) {
-  if (tiling == kDecodeListTiles)
+                           int tiling, uint32_t grid, uint32_t lds, hipStream_t s,
+                           const ArgItems* args) {
+  if (tiling == kDecodeArgListTiles)
+    decode_arglist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
+        static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p), g, *args);
+  else if (tiling == kDecodeListTiles)
     decode_list_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
         static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p),
         reinterpret_cast<const uint32_t*>(bm), g);
@@ -406,8 +431,9 @@ hipError_t enc_nm(const void* d, void* p, const Geometry& g, uint32_t grid, uint
 
 template <int U, bool NT, int T>
 hipError_t dec_nm(void* d, const void* p, const uint8_t* bm, const Geometry& g, int tiling,
-                  uint32_t grid, uint32_t lds, hipStream_t s) {
-  XEC_NM_SWITCH(g.nm, return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, tiling, grid, lds, s)))
+                  uint32_t grid, uint32_t lds, hipStream_t s, const ArgItems* a) {
+  XEC_NM_SWITCH(g.nm,
+                return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, tiling, grid, lds, s, a)))
 }
 
 template <bool NT, int T>
@@ -419,9 +445,9 @@ hipError_t enc_u(const void* d, void* p, const Geometry& g, int unroll, uint32_t
 
 template <bool NT, int T>
 hipError_t dec_u(void* d, const void* p, const uint8_t* bm, const Geometry& g, int tiling,
-                 int unroll, uint32_t grid, uint32_t lds, hipStream_t s) {
-  return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, tiling, grid, lds, s)
-                     : dec_nm<1, NT, T>(d, p, bm, g, tiling, grid, lds, s);
+                 int unroll, uint32_t grid, uint32_t lds, hipStream_t s, const ArgItems* a) {
+  return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, tiling, grid, lds, s, a)
+                     : dec_nm<1, NT, T>(d, p, bm, g, tiling, grid, lds, s, a);
 }
 
 }  // namespace
@@ -439,23 +465,34 @@ hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
 
 hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bitmap,
                          const Geometry& g_class, const LaunchShape& ls, int tiling,
-                         hipStream_t s, uint64_t n_items) {
+                         hipStream_t s, uint64_t n_items, const uint32_t* h_items) {
   // stripe tiles (stripe, chunk): decode_kernel; class tiles (stripe, class,
   // chunk) = encode's tiling: decode_class_kernel (with m == 1 the two
   // coincide and the stripe kernel runs); list tiles (entry, chunk):
-  // decode_list_kernel over the n_items entries d_bitmap holds.
+  // decode_list_kernel over the n_items entries d_bitmap holds, or
+  // decode_arglist_kernel over h_items (<= kArgItems) passed by value.
   Geometry g = g_class;
   if (tiling == kDecodeClassTiles && g.m <= 1) tiling = kDecodeStripeTiles;
   if (tiling == kDecodeStripeTiles) g.total_tiles = g.S * g.tiles_per_block;
-  if (tiling == kDecodeListTiles) g.total_tiles = n_items * g.tiles_per_block;
+  if (tiling == kDecodeListTiles || tiling == kDecodeArgListTiles)
+    g.total_tiles = n_items * g.tiles_per_block;
   if (g.total_tiles == 0) return hipSuccess;
+  ArgItems args;
+  if (tiling == kDecodeArgListTiles) {
+    if (n_items > kArgItems || h_items == nullptr) return hipErrorInvalidValue;
+    std::memcpy(args.v, h_items, n_items * sizeof(uint32_t));
+  }
+  const ArgItems* a = tiling == kDecodeArgListTiles ? &args : nullptr;
   const uint32_t grid = grid_for(g.total_tiles, ls.max_grid, ls.threads);
   const uint32_t lds = ls.lds_bytes;
   if (ls.threads == 256)
-    return ls.nt ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s)
-                 : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s);
-  return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s)
-               : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s);
+    return ls.nt
+               ? dec_u<true, 256>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s, a)
+               : dec_u<false, 256>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s,
+                                   a);
+  return ls.nt ? dec_u<true, 64>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s, a)
+               : dec_u<false, 64>(d_data, d_parity, d_bitmap, g, tiling, ls.unroll, grid, lds, s,
+                                  a);
 }
 
 hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,

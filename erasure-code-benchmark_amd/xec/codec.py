@@ -116,6 +116,17 @@ def set_validate_kernel(mode: int = 0) -> Status:
     return Status(lib().xec_set_validate_kernel(mode))
 
 
+#: xec_decode_tiling_used values (include/xec.h)
+DECODE_KERNELS = {1: "xec::decode_kernel", 2: "xec::decode_class_kernel",
+                  3: "xec::decode_list_kernel", 4: "xec::decode_arglist_kernel"}
+
+
+def decode_tiling_used() -> int:
+    """xec_decode_tiling_used: the tiling this thread's last xec_decode launched
+    (0 none, 1 stripe, 2 class, 3 device list, 4 kernel-argument list)."""
+    return int(lib().xec_decode_tiling_used())
+
+
 def status_string(st: int) -> str:
     return lib().xec_status_string(int(st)).decode()
 

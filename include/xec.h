@@ -72,11 +72,11 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * (require_recovery, xorec_utils.hpp:144-149).  Otherwise every lost data
  * block is rebuilt:
  *   data[c][i] = parity[c][i%m] ^ XOR_{l%m == i%m, l != i} data[c][l].
- * d_bitmap is scratch for the call: it receives on `stream` a copy of
+ * d_bitmap is scratch for the call: it may receive on `stream` a copy of
  * h_bitmap and/or the list of lost data blocks the host scan found (4 bytes
- * each; used when at most 3/4 of the stripes lost a data block and the list
- * fits in its S*(k+m) bytes, k <= 256, S <= 2^24: one tile per lost block and
- * 1 KiB chunk, xec_set_decode_tiling).
+ * each).  The list drives one tile per lost block and 1 KiB chunk
+ * (xec_set_decode_tiling); up to 1,024 entries travel in the kernel
+ * arguments instead, and then nothing is copied.
  * Lost parity is not regenerated.  Parity is READ-ONLY here, as in the CPU
  * decode (xorec.cpp:62-111) -- deliberately unlike the reference GPU decode,
  * which folds all data into parity (xorec_gpu_cmp.cu:94-102).  The content of
@@ -169,7 +169,8 @@ xec_status xec_set_occupancy(int waves_per_simd);
  * batch.  0 = automatic (default): work-list tiles -- one per (lost data
  * block, 1 KiB column chunk), from the list the host scan builds -- when at
  * most 3/4 of the stripes lost a data block and the list fits the scratch
- * (see xec_decode); otherwise class tiles -- one
+ * (k <= 256, S <= 2^24), and for lists of up to 1,024 entries wherever
+ * stripe tiles would run; otherwise class tiles -- one
  * per (stripe, class, chunk), one class reduction each, encode's tiling --
  * when the batch lost more than one data block per stripe on average and at
  * least half of its S*m classes lost one, else stripe tiles -- one per
@@ -190,6 +191,16 @@ xec_status xec_set_decode_tiling(int tiling);
  * 1 = always lane per block, 2 = grouped wherever bs allows it.  Results are
  * identical.  XEC_INVALID_SIZE outside 0..2. */
 xec_status xec_set_validate_kernel(int mode);
+
+/* Diagnostics: which tiling the calling thread's most recent xec_decode
+ * launched -- 0 none (an error, or nothing to rebuild), then one of: */
+enum {
+  XEC_TILING_STRIPE = 1,   /* decode_kernel: (stripe, chunk) tiles over the bitmap */
+  XEC_TILING_CLASS = 2,    /* decode_class_kernel: (stripe, class, chunk) tiles */
+  XEC_TILING_LIST = 3,     /* decode_list_kernel: (lost block, chunk), list in d_bitmap */
+  XEC_TILING_ARG_LIST = 4  /* decode_arglist_kernel: the same, list in the kernel arguments */
+};
+int xec_decode_tiling_used(void);
 
 /* ---- host-in / host-out pipeline --------------------
  * The MI355X analogue of the reference's GPU-memory / unified-memory variants

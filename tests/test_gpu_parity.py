@@ -234,6 +234,8 @@ def test_encode_is_linear(gpu):
     (64, 16, 4, 4096, "sparse"),    # a few stripes lost a block, most none
     (64, 16, 8, 2048, "skew"),      # some stripes lost a block in every class, the rest none
     (3, 264, 8, 256, "all"),        # k > 256: no work list, bitmap path
+    (2048, 4, 1, 256, "one"),       # 2,048 lost blocks: past the kernel-argument list (1,024)
+    (4096, 8, 4, 256, "half"),      # 8,192: a device-memory list under tiling 3
     (40, 32, 8, 4352, "all"),       # ragged tail tile
     (33, 8, 2, 2048, "all"),
     (50, 16, 4, 4096, "half"),      # half the classes: class tiles with idle tiles (auto)
@@ -314,3 +316,46 @@ def test_grid_beyond_hip_launch_limit(gpu):
     assert torch.equal(d, p)
     del d, p
     torch.cuda.empty_cache()
+
+
+def _pattern(kind, S, k, m, rng):
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(S):
+        if kind == "one" or (kind == "sparse" and c % 9 == 4):
+            bm[c, (7 * c) % k] = 0
+        elif kind == "all":
+            for j in range(m):
+                bm[c, j + m * int(rng.integers(k // m))] = 0
+        elif kind == "parity_only":
+            bm[c, k] = 0
+        elif kind == "double":
+            if c == S // 2:
+                bm[c, 0] = bm[c, m] = 0  # two losses in class 0: DecodeFailure
+    return bm
+
+
+@pytest.mark.parametrize("S,k,m,bs,kind,tiling,want", [
+    (16, 16, 1, 65536, "one", 0, 4),      # 16 lost blocks: list in the kernel arguments
+    (1024, 8, 1, 4096, "one", 0, 4),      # exactly kArgItems entries
+    (2048, 4, 1, 256, "one", 0, 1),       # 2,048, every stripe: stripe tiles
+    (18432, 4, 1, 256, "sparse", 0, 3),   # 2,048 lost, 1 stripe in 9: device list
+    (2048, 4, 1, 256, "sparse", 0, 4),    # 228 lost, 1 in 9: kernel arguments
+    (64, 16, 2, 4096, "all", 0, 2),       # every class lost a block: class tiles
+    (600, 8, 4, 256, "all", 0, 2),
+    (16, 16, 1, 65536, "one", 1, 1),      # forced stripe tiles
+    (64, 16, 2, 4096, "all", 3, 4),       # forced list: 128 entries in the arguments
+    (16, 16, 1, 65536, "parity_only", 0, 0),  # nothing to rebuild: no launch
+    (64, 8, 2, 1024, "double", 0, 0),     # DecodeFailure: no launch
+])
+def test_decode_tiling_policy(gpu, oracle, S, k, m, bs, kind, tiling, want):
+    """xec_decode_tiling_used: the automatic policy of include/xec.h picks the
+    kernel it documents, and every pick rebuilds bit-exactly."""
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    bm = _pattern(kind, S, k, m, np.random.default_rng(S + k))
+    assert gpu.set_decode_tiling(tiling) == gpu.Status.SUCCESS
+    try:
+        expect = gpu.Status.DECODE_FAILURE if kind == "double" else gpu.Status.SUCCESS
+        erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1), expect=expect)
+        assert gpu.decode_tiling_used() == want
+    finally:
+        gpu.set_decode_tiling(0)

@@ -3,9 +3,12 @@
 //   latency <mode 0..3> [k m bs S iters]
 // mode: 0 default, 1 spin, 2 yield, 3 blocking sync -- set with
 // hipSetDeviceFlags BEFORE any other HIP call (afterwards it is ignored).
-// Prints median/p10/p90 microseconds for: an empty kernel + stream sync,
-// xec_encode + stream sync, xec_encode + event sync, and a captured hipGraph
-// holding the encode + graph sync.
+// Prints median/p10/p90 microseconds for: an empty kernel + stream sync, one
+// whose arguments are ~4 KB (what passing a decode work list by value would
+// cost), xec_encode + stream sync, xec_encode + event sync, a captured
+// hipGraph holding the encode + graph sync, and xec_decode (one lost data
+// block per stripe, pinned host bitmap) + stream sync with the automatic and
+// the work-list tiling.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,6 +20,14 @@
 #include "xec.h"
 
 __global__ void empty_kernel() {}
+
+struct BigArgs {
+  uint32_t n;
+  uint32_t v[1000];
+};
+__global__ void bigarg_kernel(BigArgs a, uint32_t* out) {
+  if (threadIdx.x == 0) out[0] = a.v[a.n % 1000];
+}
 
 static void report(const char* name, std::vector<double>& us) {
   std::sort(us.begin(), us.end());
@@ -67,6 +78,28 @@ int main(int argc, char** argv) {
   }
   report("empty kernel + stream sync", t);
   t.clear();
+  {
+    static BigArgs ba;
+    ba.n = 7;
+    for (int i = 0; i < 1000; ++i) ba.v[i] = i;
+    uint32_t* dout;
+    CK(hipMalloc(&dout, 4));
+    for (int i = 0; i < iters + 50; ++i) {
+      auto t0 = clk::now();
+      ba.n = i;
+      bigarg_kernel<<<1, 64, 0, s>>>(ba, dout);
+      CK(hipStreamSynchronize(s));
+      if (i >= 50) t.push_back(us_since(t0));
+    }
+    uint32_t hv = 0;
+    CK(hipMemcpy(&hv, dout, 4, hipMemcpyDeviceToHost));
+    if (hv != (uint32_t)((iters + 49) % 1000)) {
+      std::fprintf(stderr, "bigarg kernel read %u\n", hv);
+      return 3;
+    }
+    report("4 KB-arg kernel + stream sync", t);
+    t.clear();
+  }
   for (int i = 0; i < iters + 50; ++i) {
     auto t0 = clk::now();
     if (xec_encode(d, p, S, bs, k, m, s) != XEC_SUCCESS) return 2;
@@ -114,5 +147,25 @@ int main(int argc, char** argv) {
     t.push_back(ms * 1e3);
   }
   report("encode device time (events)", t);
+  t.clear();
+  // decode: one lost data block per stripe, (7c) mod k (bench.py's pattern)
+  uint8_t* h_bm;
+  uint8_t* d_bm;
+  CK(hipHostMalloc(reinterpret_cast<void**>(&h_bm), S * (k + m), hipHostMallocDefault));
+  CK(hipMalloc(reinterpret_cast<void**>(&d_bm), S * (k + m)));
+  for (size_t c = 0; c < S; ++c)
+    for (size_t i = 0; i < k + m; ++i) h_bm[c * (k + m) + i] = i == (7 * c) % k ? 0 : 1;
+  for (int tiling : {0, 3}) {
+    if (xec_set_decode_tiling(tiling) != XEC_SUCCESS) return 2;
+    for (int i = 0; i < iters + 50; ++i) {
+      auto t0 = clk::now();
+      if (xec_decode(d, p, S, bs, k, m, h_bm, d_bm, s) != XEC_SUCCESS) return 2;
+      CK(hipStreamSynchronize(s));
+      if (i >= 50) t.push_back(us_since(t0));
+    }
+    report(tiling ? "xec_decode list + sync" : "xec_decode auto + sync", t);
+    t.clear();
+  }
+  xec_set_decode_tiling(0);
   return 0;
 }

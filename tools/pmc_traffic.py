@@ -57,7 +57,8 @@ def main():
     k, m, bs, S, _ = workload_shape(workload)
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
     algo = {"xec::encode_kernel": b_enc, "xec::decode_kernel": b_dec * lost,
-            "xec::decode_class_kernel": b_dec * lost}
+            "xec::decode_class_kernel": b_dec * lost, "xec::decode_list_kernel": b_dec * lost,
+            "xec::decode_arglist_kernel": b_dec * lost}
 
     kernels = {}
     for name in sorted(set(fetch) & set(write)):
@@ -92,6 +93,7 @@ def main():
         dec = [v for n, v in kernels.items() if n.startswith("xec::decode")]
         if dec:
             traffic["decode_hbm_bytes_per_launch"] = dec[0]["hbm_bytes_per_launch"]
+            traffic["decode_kernel"] = [n for n in kernels if n.startswith("xec::decode")][0]
         (dst / f"traffic_{workload}.json").write_text(json.dumps(traffic, indent=1) + "\n")
     print(json.dumps(out, indent=1))
 
