@@ -338,6 +338,57 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
 
 int xec_decode_tiling_used(void) { return g_tiling_used; }
 
+xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, size_t bs,
+                                 size_t k, size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
+                                 uint8_t* h_codes, hipStream_t stream) {
+  g_tiling_used = 0;
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
+  if (st != XEC_SUCCESS) return st;
+  if (S == 0) return XEC_SUCCESS;
+  if (k > kWorkItemMaxK || S > kWorkItemMaxStripes) return XEC_INVALID_SIZE;
+  uint64_t n = 0, failures = 0;
+  st = xec_scan_stripes(h_bitmap, S, k, m, h_codes, nullptr, 0, &n, &failures);
+  if (st != XEC_SUCCESS) return st;
+  const xec_status verdict = failures ? XEC_DECODE_FAILURE : XEC_SUCCESS;
+  if (n == 0) return verdict;
+  const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+  const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+  if (n <= xec::kArgItems) {
+    uint32_t items[xec::kArgItems];
+    (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, xec::kArgItems, &n, &failures);
+    g_tiling_used = XEC_TILING_ARG_LIST;
+    return xec::launch_decode(d_data, d_parity, nullptr, g, ls, xec::kDecodeArgListTiles, stream,
+                              n, items) == hipSuccess
+               ? verdict
+               : XEC_DEVICE_ERROR;
+  }
+  // A longer list goes through the scratch in pieces of what it holds: copy
+  // a piece, rebuild it, copy the next (stream order keeps a copy behind the
+  // kernel still reading the previous piece).
+  const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
+  const uint64_t cap = (S * (k + m) - pad) / 4;  // >= 511 here: n > 1,024 <= S*k
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
+  Staging* sg = stage_acquire(n * 4, dev);
+  if (sg == nullptr) return XEC_DEVICE_ERROR;
+  uint32_t* items = static_cast<uint32_t*>(sg->host);
+  (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, n, &n, &failures);
+  uint8_t* d_items = d_bitmap + pad;
+  bool queued = false, ok = true;
+  for (uint64_t q0 = 0; q0 < n && ok; q0 += cap) {
+    const uint64_t piece = n - q0 < cap ? n - q0 : cap;
+    ok = hipMemcpyAsync(d_items, items + q0, piece * 4, hipMemcpyHostToDevice, stream) ==
+         hipSuccess;
+    queued |= ok;
+    ok = ok && xec::launch_decode(d_data, d_parity, d_items, g, ls, xec::kDecodeListTiles, stream,
+                                  piece) == hipSuccess;
+  }
+  stage_release(sg, queued, stream);
+  g_tiling_used = XEC_TILING_LIST;
+  return ok ? verdict : XEC_DEVICE_ERROR;
+}
+
 xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                              size_t m, const uint8_t* d_bitmap, int32_t* d_status,
                              hipStream_t stream) {

@@ -29,3 +29,12 @@ struct XecScan {
 // xec_scan.cpp.
 xec_status xec_scan_bitmap(const uint8_t* h_bitmap, size_t S, size_t k, size_t m, XecScan* out,
                            uint32_t* items, uint64_t cap);
+
+// Per-stripe form (the reference CPU plugin's loop, xorec_bm.cpp:43-58 over
+// xorec_decode, xorec.cpp:62-111): codes[c] (if non-null) = 0 or 4
+// (DecodeFailure) for every stripe; *failures = stripes with 4; work items
+// (first `cap` to `items`) and *n_items only for stripes that need recovery
+// and are recoverable.  XEC_INVALID_COUNTS as xec_check_args, else success.
+xec_status xec_scan_stripes(const uint8_t* h_bitmap, size_t S, size_t k, size_t m,
+                            uint8_t* codes, uint32_t* items, uint64_t cap, uint64_t* n_items,
+                            uint64_t* failures);

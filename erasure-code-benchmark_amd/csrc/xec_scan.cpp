@@ -180,7 +180,116 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
 }
 #endif
 
+// ---- per-stripe verdicts (xec_decode_per_stripe) ---------------------------
+// The reference CPU plugin decodes stripe by stripe (xorec_bm.cpp:43-58): an
+// unrecoverable stripe fails alone and the others are rebuilt.  One verdict
+// per stripe, and work items only for the stripes that are rebuilt.
+struct StripeScan {
+  uint8_t* codes;   // S verdicts (0 / 4), may be null
+  uint32_t* items;  // may be null
+  uint64_t cap;
+  uint64_t n = 0, failures = 0;
+  inline void emit(size_t c, uint64_t zd) {
+    for (; zd; zd &= zd - 1, ++n)
+      if (n < cap) items[n] = xec_work_item(c, static_cast<size_t>(__builtin_ctzll(zd)));
+  }
+};
+
+void stripes_scalar(const uint8_t* bm, size_t S, size_t k, size_t m, StripeScan& o) {
+  const size_t row = k + m;
+  std::vector<uint8_t> hit(m);
+  for (size_t c = 0; c < S; ++c) {
+    const uint8_t* r = bm + c * row;
+    bool need = false;
+    for (size_t i = 0; i < k; ++i) need |= !(r[i] & 1u);  // require_recovery
+    uint8_t code = 0;
+    if (need) {  // is_recoverable: at most one zero byte per class
+      for (size_t j = 0; j < m; ++j) hit[j] = r[k + j] == 0;
+      for (size_t i = 0; i < k && code == 0; ++i)
+        if (r[i] == 0) {
+          if (hit[i % m]) code = 4;
+          hit[i % m] = 1;
+        }
+      if (code == 0)
+        for (size_t i = 0; i < k; ++i)
+          if (r[i] == 0) {
+            if (o.n < o.cap) o.items[o.n] = xec_work_item(c, i);
+            ++o.n;
+          }
+    }
+    o.failures += code != 0;
+    if (o.codes) o.codes[c] = code;
+  }
+}
+
+#if defined(__x86_64__)
+__attribute__((target("avx2,bmi,popcnt"))) void stripes_avx2(const uint8_t* bm, size_t S,
+                                                            size_t k, size_t m, StripeScan& o) {
+  const size_t row = k + m;
+  const uint64_t row_mask = row == 64 ? ~0ull : ((1ull << row) - 1);
+  const uint64_t data_mask = (1ull << k) - 1;
+  uint8_t cls[64];
+  for (size_t i = 0; i < row; ++i) cls[i] = static_cast<uint8_t>(i < k ? i % m : i - k);
+  const __m256i one = _mm256_set1_epi8(1), zero = _mm256_setzero_si256();
+  const size_t n = S * row;
+  alignas(32) uint8_t pad[64];
+  for (size_t c = 0; c < S; ++c) {
+    const uint8_t* r = bm + c * row;
+    if (c * row + 64 > n) {
+      std::memset(pad, 1, sizeof pad);
+      std::memcpy(pad, r, row);
+      r = pad;
+    }
+    const __m256i x0 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(r));
+    const __m256i x1 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(r + 32));
+    const uint64_t z =
+        (static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(x0, zero))) |
+         static_cast<uint64_t>(static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(x1, zero)))) << 32) &
+        row_mask;
+    const uint64_t e =
+        (static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_and_si256(x0, one), zero))) |
+         static_cast<uint64_t>(static_cast<uint32_t>(
+             _mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_and_si256(x1, one), zero)))) << 32);
+    uint8_t code = 0;
+    if (e & data_mask) {
+      if (z & (z - 1)) {
+        uint64_t seen = 0, bits = z;
+        for (; bits; bits &= bits - 1) {
+          const uint64_t bit = 1ull << cls[__builtin_ctzll(bits)];
+          if (seen & bit) {
+            code = 4;
+            break;
+          }
+          seen |= bit;
+        }
+      }
+      if (code == 0) o.emit(c, z & data_mask);
+    }
+    o.failures += code != 0;
+    if (o.codes) o.codes[c] = code;
+  }
+}
+#endif
+
 }  // namespace
+
+xec_status xec_scan_stripes(const uint8_t* bm, size_t S, size_t k, size_t m, uint8_t* codes,
+                            uint32_t* items, uint64_t cap, uint64_t* n_items,
+                            uint64_t* failures) {
+  if (k < 1 || m < 1 || k % m != 0) return XEC_INVALID_COUNTS;
+  StripeScan o{codes, items, items ? cap : 0};
+#if defined(__x86_64__)
+  static const bool fast = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi") &&
+                           __builtin_cpu_supports("popcnt");
+  if (fast && k + m <= 64 && S > 0)
+    stripes_avx2(bm, S, k, m, o);
+  else
+#endif
+    stripes_scalar(bm, S, k, m, o);
+  if (n_items) *n_items = o.n;
+  if (failures) *failures = o.failures;
+  return XEC_SUCCESS;
+}
 
 // Also counts the zero (lost) data bytes and the stripes that have one and,
 // when `items` is given, lists the first `cap` of them in batch order

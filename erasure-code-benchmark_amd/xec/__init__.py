@@ -6,14 +6,16 @@ multi-GPU partitioning helpers; it never computes parity itself.
 """
 from ._lib import EXPORTED, LIB_PATH, Status, XecLibraryError, lib
 from .codec import (DECODE_KERNELS, Pipeline, build_info, check_args, check_bitmap, decode,
-                    decode_device, decode_tiling_used, encode, erase, fill_splitmix64, init,
+                    decode_device, decode_per_stripe, decode_tiling_used, encode, erase,
+                    fill_splitmix64, init,
                     set_decode_tiling, set_launch, set_occupancy, set_validate_kernel,
                     status_string, validate_blocks, write_validation_pattern)
 from .partition import stripe_range
 
 __all__ = [
     "DECODE_KERNELS", "EXPORTED", "LIB_PATH", "Pipeline", "Status", "XecLibraryError", "lib",
-    "build_info", "check_args", "check_bitmap", "decode", "decode_device", "decode_tiling_used",
+    "build_info", "check_args", "check_bitmap", "decode", "decode_device", "decode_per_stripe",
+    "decode_tiling_used",
     "encode", "erase", "fill_splitmix64", "init", "set_decode_tiling", "set_launch",
     "set_occupancy", "set_validate_kernel", "status_string", "stripe_range", "validate_blocks",
     "write_validation_pattern",

@@ -26,7 +26,7 @@ EXPORTED = (
     "xec_build_info", "xec_pipeline_create", "xec_pipeline_destroy", "xec_pipeline_encode",
     "xec_pipeline_decode", "xec_write_validation_pattern", "xec_validate_blocks",
     "xec_decode_device", "xec_set_occupancy", "xec_set_decode_tiling",
-    "xec_set_validate_kernel", "xec_decode_tiling_used",
+    "xec_set_validate_kernel", "xec_decode_tiling_used", "xec_decode_per_stripe",
 )
 
 
@@ -83,6 +83,7 @@ def lib() -> ctypes.CDLL:
         "xec_set_decode_tiling": ([ctypes.c_int], st),
         "xec_set_validate_kernel": ([ctypes.c_int], st),
         "xec_decode_tiling_used": ([], ctypes.c_int),
+        "xec_decode_per_stripe": ([vp, vp, sz, sz, sz, sz, vp, vp, vp, vp], st),
         "xec_status_string": ([st], ctypes.c_char_p),
         "xec_build_info": ([], ctypes.c_char_p),
         "xec_pipeline_create": ([ctypes.POINTER(vp), sz, sz, sz, sz, ctypes.c_int], st),

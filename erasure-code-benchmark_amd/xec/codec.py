@@ -48,6 +48,17 @@ def decode(d_data, d_parity, S: int, bs: int, k: int, m: int, h_bitmap, d_bitmap
                                    _ptr(d_bitmap), _stream(stream)))
 
 
+def decode_per_stripe(d_data, d_parity, S: int, bs: int, k: int, m: int, h_bitmap, d_bitmap,
+                      h_codes=None, stream=None) -> Status:
+    """xec_decode_per_stripe -- the reference CPU plugin's per-stripe semantics
+    (xorec_bm.cpp:43-58): recoverable stripes are rebuilt, unrecoverable ones
+    left alone; h_codes (S host bytes, optional) gets each stripe's 0 / 4."""
+    return Status(lib().xec_decode_per_stripe(_ptr(d_data), _ptr(d_parity), S, bs, k, m,
+                                              _ptr(h_bitmap), _ptr(d_bitmap),
+                                              _ptr(h_codes) if h_codes is not None else None,
+                                              _stream(stream)))
+
+
 def decode_device(d_data, d_parity, S: int, bs: int, k: int, m: int, d_bitmap, d_status,
                   stream=None) -> Status:
     """xec_decode_device -- bitmap already on the device; batch verdict lands in

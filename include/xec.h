@@ -89,6 +89,20 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                       size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream);
 
+/* Per-stripe form of xec_decode: the semantics of the reference CPU plugin
+ * (XorecBenchmark::decode, xorec_bm.cpp:43-58, xorec_decode per stripe,
+ * xorec.cpp:62-111) rather than of its GPU path.  Every stripe that needs
+ * recovery and is recoverable is rebuilt; an unrecoverable stripe is left
+ * untouched and makes the call return XEC_DECODE_FAILURE after the others
+ * are queued.  h_codes (S bytes of host memory, may be NULL) receives each
+ * stripe's XorecResult (0, or 4 for that stripe), written before the call
+ * returns.  Always work-list tiles (one per rebuilt block and 1 KiB chunk);
+ * requires k <= 256 and S <= 2^24 (else XEC_INVALID_SIZE).  Other arguments,
+ * checks and the scratch as xec_decode. */
+xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, size_t bs,
+                                 size_t k, size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
+                                 uint8_t* h_codes, hipStream_t stream);
+
 /* Device-resident form of xec_decode (no reference counterpart: the reference
  * always scans a host bitmap, xorec_gpu_cmp.cu:75-83).  For callers whose
  * erasure bitmap already lives in device memory: no host scan, no copy, no

@@ -74,8 +74,32 @@ int main() {
     if (items != nullptr && got2 == XEC_SUCCESS)
       for (uint64_t q = 0; q < cap; ++q) items_ok &= items[q] == items_ref[q];
     delete[] items;
+    std::vector<uint8_t> bm_keep(bm, bm + n);
     delete[] bm;
-    if (!items_ok || !stripes_ok) {
+    // per-stripe form: codes and the items of recoverable stripes only
+    std::vector<uint8_t> codes(S ? S : 1, 0xAA), codes_ref(S ? S : 1, 0);
+    std::vector<uint32_t> ps_ref;
+    for (size_t c = 0; c < S; ++c) {
+      int nd = 0;
+      const int st_c = reference(bm_keep.data() + c * (k + m), 1, k, m, &nd);
+      codes_ref[c] = nd && st_c != XEC_SUCCESS ? 4 : 0;
+      if (nd && st_c == XEC_SUCCESS)
+        for (size_t i = 0; i < k; ++i)
+          if (bm_keep[c * (k + m) + i] == 0) ps_ref.push_back(static_cast<uint32_t>(c << 8 | i));
+    }
+    bool ps_ok = true;
+    if (k <= 256) {
+      std::vector<uint32_t> ps(ps_ref.size() + 1);
+      uint64_t n_ps = 0, fails = 0;
+      ps_ok = xec_scan_stripes(bm_keep.data(), S, k, m, codes.data(), ps.data(), ps.size(), &n_ps,
+                               &fails) == XEC_SUCCESS;
+      uint64_t fails_ref = 0;
+      for (size_t c = 0; c < S; ++c) fails_ref += codes_ref[c] != 0;
+      ps_ok = ps_ok && n_ps == ps_ref.size() && fails == fails_ref;
+      for (size_t c = 0; ps_ok && c < S; ++c) ps_ok = codes[c] == codes_ref[c];
+      for (size_t q = 0; ps_ok && q < ps_ref.size(); ++q) ps_ok = ps[q] == ps_ref[q];
+    }
+    if (!items_ok || !stripes_ok || !ps_ok) {
       std::printf("WORK LIST MISMATCH trial %d k=%zu m=%zu S=%zu\n", trial, k, m, S);
       return 1;
     }

@@ -359,3 +359,58 @@ def test_decode_tiling_policy(gpu, oracle, S, k, m, bs, kind, tiling, want):
         assert gpu.decode_tiling_used() == want
     finally:
         gpu.set_decode_tiling(0)
+
+
+def test_golden_decode_fixtures_per_stripe(gpu, oracle, known_answers):
+    """xec_decode_per_stripe reproduces the reference CPU plugin's per-stripe
+    decode (xorec_bm.cpp:43-58) bit for bit, failing stripes included: the
+    per-stripe codes and the data / parity hashes after decode are the ones the
+    reference itself produced (tests/golden/make_golden.py)."""
+    torch = _torch()
+    for e in known_answers["decode"]:
+        k, m, bs, S = e["k"], e["m"], e["bs"], e["S"]
+        bm = np.fromfile(GOLDEN / "patterns" / e["pattern"], dtype=np.uint8)
+        b, _, _ = encode_and_check(gpu, oracle, S, k, m, bs, known_answers["seed"])
+        h_bm = torch.from_numpy(bm).pin_memory()
+        d_bm = h_bm.to("cuda")
+        assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == gpu.Status.SUCCESS
+        codes = np.full(S, 0xAA, np.uint8)
+        st = gpu.decode_per_stripe(b.d, b.p, S, bs, k, m, h_bm, torch.empty_like(d_bm), codes,
+                                   b.stream)
+        want = [int(x) for x in e["codes"]]
+        assert codes.tolist() == want, e["mode"]
+        assert st == (gpu.Status.DECODE_FAILURE if 4 in want else gpu.Status.SUCCESS), e["mode"]
+        assert f"{oracle.fnv1a64(b.data()):016x}" == e["data_fnv_after"], e["mode"]
+        assert f"{oracle.fnv1a64(b.parity()):016x}" == e["parity_fnv_after"], e["mode"]
+
+
+@pytest.mark.parametrize("S,k,m,bs", [(4096, 4, 2, 256), (300, 16, 4, 1024), (5000, 8, 8, 256)])
+def test_per_stripe_long_lists_and_failures(gpu, oracle, S, k, m, bs):
+    """More rebuilt blocks than the kernel arguments carry, and than the
+    scratch holds at once (k/m small: the list goes through it in pieces);
+    every 7th stripe unrecoverable and left exactly as erased."""
+    torch = _torch()
+    b, ref_d, _ = encode_and_check(gpu, oracle, S, k, m, bs)
+    rng = np.random.default_rng(S * 31 + k)
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(S):
+        for j in range(m):
+            bm[c, j + m * int(rng.integers(k // m))] = 0
+        if c % 7 == 3:
+            bm[c, k + int(rng.integers(m))] = 0  # data and parity of one class: DecodeFailure
+    h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
+    d_bm = h_bm.to("cuda")
+    assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == gpu.Status.SUCCESS
+    erased = b.data().reshape(S, k * bs).copy()
+    codes = np.zeros(S, np.uint8)
+    st = gpu.decode_per_stripe(b.d, b.p, S, bs, k, m, h_bm, torch.empty_like(d_bm), codes,
+                               b.stream)
+    assert st == gpu.Status.DECODE_FAILURE
+    bad = np.arange(S) % 7 == 3
+    assert (codes[bad] == 4).all() and (codes[~bad] == 0).all()
+    got = b.data().reshape(S, k * bs)
+    assert np.array_equal(got[~bad], ref_d.reshape(S, k * bs)[~bad])
+    assert np.array_equal(got[bad], erased[bad])
+    n_rebuilt = int((bm[~bad, :k] == 0).sum())
+    assert n_rebuilt > 1024
+    assert gpu.decode_tiling_used() == 3
