@@ -199,6 +199,23 @@ xec::LaunchShape launch_shape(size_t bs, int auto_w) {
   return ls;
 }
 
+// Workgroups the chip holds at once for a launch of shape ls (CUs x the
+// workgroups per CU its LDS reservation admits, at most 32 waves per CU):
+// the fixed grid of decode_devlist_kernel, which walks a count the host never
+// sees.  0 if the device cannot be queried.
+uint32_t resident_workgroups(const xec::LaunchShape& ls) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return 0;
+  const uint32_t waves = (uint32_t)ls.threads / 64u;
+  uint32_t per_cu = 32u / (waves ? waves : 1u);
+  if (ls.lds_bytes > 0 && (160u * 1024u) / ls.lds_bytes < per_cu)
+    per_cu = (160u * 1024u) / ls.lds_bytes;
+  return (uint32_t)cus * (per_cu ? per_cu : 1u);
+}
+
 }  // namespace
 
 extern "C" {
@@ -412,6 +429,43 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
   return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls,
                             cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
                             stream) == hipSuccess
+             ? XEC_SUCCESS
+             : XEC_DEVICE_ERROR;
+}
+
+size_t xec_decode_device_list_bytes(size_t S, size_t k, size_t m) {
+  (void)k;
+  return 4 * (xec::kDevListHeader + S * m);
+}
+
+xec_status xec_decode_device_list(void* d_data, const void* d_parity, size_t S, size_t bs,
+                                  size_t k, size_t m, const uint8_t* d_bitmap, void* d_work,
+                                  size_t work_bytes, int32_t* d_status, hipStream_t stream) {
+  if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
+  xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
+  if (st != XEC_SUCCESS) return st;
+  // every argument is checked before any work is queued on the stream
+  if (d_status == nullptr || reinterpret_cast<uintptr_t>(d_status) % 4 != 0 ||
+      d_work == nullptr || reinterpret_cast<uintptr_t>(d_work) % 4 != 0)
+    return XEC_INVALID_ALIGNMENT;
+  if (S != 0 && (d_bitmap == nullptr || k > kWorkItemMaxK || S > kWorkItemMaxStripes ||
+                 work_bytes < xec_decode_device_list_bytes(S, k, m)))
+    return XEC_INVALID_SIZE;
+  if (S == 0)
+    return hipMemsetAsync(d_status, 0, sizeof(int32_t), stream) == hipSuccess ? XEC_SUCCESS
+                                                                              : XEC_DEVICE_ERROR;
+  // one reduction per tile, as encode: encode's residency table; the grid is
+  // what the chip holds at once unless xec_set_launch gave max_grid
+  xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+  if (ls.max_grid == 0) ls.max_grid = resident_workgroups(ls);
+  if (ls.max_grid == 0) return XEC_DEVICE_ERROR;
+  xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+  uint32_t* list = static_cast<uint32_t*>(d_work);
+  if (xec::launch_scan_list(d_bitmap, g, d_status, list, stream) != hipSuccess)
+    return XEC_DEVICE_ERROR;
+  g.gate = d_status;
+  return xec::launch_decode(d_data, d_parity, reinterpret_cast<const uint8_t*>(list), g, ls,
+                            xec::kDecodeDevListTiles, stream, S * m) == hipSuccess
              ? XEC_SUCCESS
              : XEC_DEVICE_ERROR;
 }

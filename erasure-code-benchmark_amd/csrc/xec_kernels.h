@@ -64,6 +64,16 @@ constexpr int kDecodeStripeTiles = 0;
 constexpr int kDecodeClassTiles = 1;
 constexpr int kDecodeListTiles = 2;
 constexpr int kDecodeArgListTiles = 3;
+// DevList: list tiles over a list the device built (launch_scan_list):
+// d_bitmap = the u32 list: [0] = entry count, work-queue head h at
+// [kDevListHeadStride * (1 + h)], entries from [kDevListHeader]; n_items = the
+// most entries there can be (sizes the grid with ls.max_grid; g.gate must be
+// set).
+constexpr int kDecodeDevListTiles = 4;
+constexpr uint32_t kDevListHeads = 8;        // one per XCD
+constexpr uint32_t kDevListHeadStride = 64;  // u32 words between heads (256 B)
+constexpr uint32_t kDevListGrab = 4;         // consecutive tiles of a head per pull
+constexpr uint32_t kDevListHeader = kDevListHeadStride * (kDevListHeads + 1);
 constexpr uint64_t kArgItems = 1024;
 struct ArgItems {
   uint32_t v[kArgItems];
@@ -76,6 +86,10 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
 // caller zeroes *d_status first (stream-ordered).
 hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
                         hipStream_t s);
+// The same check, and the list of lost data blocks for kDecodeDevListTiles
+// into d_list (header zeroed here with *d_status first; at most S*m entries).
+hipError_t launch_scan_list(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
+                            uint32_t* d_list, hipStream_t s);
 hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, const Geometry& g,
                         hipStream_t s);
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,

@@ -321,6 +321,122 @@ __global__ __launch_bounds__(T) void decode_arglist_kernel(uint8_t* data,
   }
 }
 
+// The same with a list the device built (xec_decode_device_list; layout in
+// xec_kernels.h kDevListHeader): the entry count is what scan_list_kernel
+// left, so the host cannot size the grid to it.  The launch is a fixed grid
+// of about what the chip holds at once, and the tiles are handed out in
+// order from work-queue heads rather than by a grid-stride walk: a
+// grid-stride walk lets each workgroup run at its own pace, so after a while
+// the tiles in flight spread over many stripes, which measured 10-18 % slower
+// than one workgroup per tile on dense batches (profiles/r02af).  With
+// H = min(8, grid) heads, workgroup b pulls from head h = b % H (round-robin
+// dispatch puts h on XCD h, so one head serves one XCD: one head word
+// saturates at ~88 dequeues/us, MI355X_MICROARCH.md, dequeue), and the q-th
+// pull of head h is tile q*H + h -- the tile one-workgroup-per-tile dispatch
+// would give that XCD next.  The next pull is issued before the current tile's
+// loads, so its latency hides behind them.  Every workgroup leaves once its
+// head runs past the count, which every head does.
+// A pull is issued by lane 0 (its value lives in lane 0 only) and handed to
+// the workgroup later, after the tile's loads and store have been issued;
+// the scheduling barriers keep the compiler from waiting on the atomic (and
+// so on the fabric round trip) before the tile's loads leave.
+__device__ __forceinline__ uint32_t devlist_issue(uint32_t* head) {
+  uint32_t q = 0;
+  // inc (wrapping at 2^32 - 1, i.e. +1 here), not add: the compiler's atomic
+  // optimizer rewrites a returning add into a wave-aggregated one whose
+  // per-lane result it computes, i.e. waits for, right away
+  if (threadIdx.x == 0) q = atomicInc(head, 0xFFFFFFFFu);
+  return q;
+}
+
+template <int T>
+__device__ __forceinline__ uint32_t devlist_bcast(uint32_t q) {
+  if constexpr (T == 64) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)q);
+  } else {
+    __shared__ uint32_t sq;
+    __syncthreads();  // every wave has read the previous pull
+    if (threadIdx.x == 0) sq = q;
+    __syncthreads();
+    return sq;
+  }
+}
+
+template <int NM, int U, bool NT, int T>
+__global__ __launch_bounds__(T) void decode_devlist_kernel(uint8_t* data,
+                                                           const uint8_t* __restrict__ parity,
+                                                           uint32_t* list, Geometry g) {
+  if (*(const_i32_as4)g.gate != 0) return;
+  const uint64_t total = (uint64_t)*(const_u32_as4)list * g.tiles_per_block;
+  const uint32_t nh = gridDim.x < kDevListHeads ? gridDim.x : kDevListHeads;
+  const uint32_t h = blockIdx.x % nh;
+  uint32_t* head = list + kDevListHeadStride * (1 + h);
+  const uint32_t* entries = list + kDevListHeader;
+  uint64_t q = devlist_bcast<T>(devlist_issue(head));
+  while ((q * kDevListGrab) * nh + h < total) {
+    const uint32_t qn = devlist_issue(head);
+    __builtin_amdgcn_sched_barrier(0);
+    for (uint32_t i = 0; i < kDevListGrab; ++i) {
+      const uint64_t t0 = (q * kDevListGrab + i) * nh + h;
+      if (t0 >= total) break;
+      const uint64_t t = total - 1 - t0;  // from the end of the list, as the other kernels
+      const uint32_t item = *(const_u32_as4)(entries + t / g.tiles_per_block);
+      rebuild_item<NM, U, NT, T>(data, parity, item, t % g.tiles_per_block, g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    q = devlist_bcast<T>(qn);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// check + list (xec_decode_device_list): one thread per (stripe, class), as
+// check_kernel, and a class that lost exactly one block, a data block, appends
+// its work item (c << 8 | i, xec_internal.h) after the list header.  A wave
+// reserves its entries with one atomicAdd on the count (ballot + popcount), so entries
+// come out grouped by wave, roughly in stripe order; their order does not
+// matter -- each entry is rebuilt on its own.  A recoverable batch has at most
+// one entry per class, so S*m entries always fit; an unrecoverable one gates
+// the decode off whatever the list holds.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void scan_list_kernel(const uint8_t* __restrict__ bitmap,
+                                                       Geometry g, int32_t* status,
+                                                       uint32_t* list) {
+  const uint64_t items = g.S * g.m, row = g.k + g.m;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256; b < items; b += (uint64_t)gridDim.x * 256) {
+    const uint64_t t = b + threadIdx.x;  // the loop is uniform per workgroup: ballot sees every lane
+    bool has = false;
+    uint32_t entry = 0;
+    if (t < items) {
+      const uint64_t c = t / g.m, j = t % g.m;
+      const uint8_t* r = bitmap + c * row;
+      uint32_t lost = r[g.k + j] == 0, li = 0;
+      for (uint64_t i = j; i < g.k; i += g.m)
+        if (r[i] == 0) {
+          ++lost;
+          li = (uint32_t)i;
+        }
+      if (lost > 1) atomicOr(status, 4 /* XEC_DECODE_FAILURE */);
+      has = lost == 1 && r[g.k + j] != 0;
+      entry = (uint32_t)(c << 8) | li;
+    }
+    const uint64_t mask = __ballot(has);
+    if (mask == 0) continue;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
+    uint32_t pos = 0;
+    if (lane == leader) pos = atomicAdd(list, (uint32_t)__popcll(mask));
+    pos = __shfl(pos, (int)leader);
+    if (has) list[kDevListHeader + pos + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = entry;
+  }
+}
+
+// *status = 0 and the list header (count, work-queue heads) = 0 in one launch,
+// stream-ordered before the scan.
+__global__ void reset_status_list_kernel(int32_t* status, uint32_t* list) {
+  if (threadIdx.x == 0) *status = 0;
+  if (threadIdx.x <= kDevListHeads) list[kDevListHeadStride * threadIdx.x] = 0u;  // count, heads
+}
+
 // ---------------------------------------------------------------------------
 // check: one thread per (stripe, class); counts the class's lost blocks among
 // its k/m data bytes and its parity byte (is_recoverable, xorec_utils.hpp:160-175).
@@ -393,7 +509,11 @@ template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
                            int tiling, uint32_t grid, uint32_t lds, hipStream_t s,
                            const ArgItems* args) {
-  if (tiling == kDecodeArgListTiles)
+  if (tiling == kDecodeDevListTiles)
+    decode_devlist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
+        static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p),
+        reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(bm)), g);
+  else if (tiling == kDecodeArgListTiles)
     decode_arglist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
         static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p), g, *args);
   else if (tiling == kDecodeListTiles)
@@ -470,11 +590,14 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
   // chunk) = encode's tiling: decode_class_kernel (with m == 1 the two
   // coincide and the stripe kernel runs); list tiles (entry, chunk):
   // decode_list_kernel over the n_items entries d_bitmap holds, or
-  // decode_arglist_kernel over h_items (<= kArgItems) passed by value.
+  // decode_arglist_kernel over h_items (<= kArgItems) passed by value;
+  // device-built list: decode_devlist_kernel over the count d_bitmap[0]
+  // holds (n_items = its upper bound, which only sizes the grid).
   Geometry g = g_class;
   if (tiling == kDecodeClassTiles && g.m <= 1) tiling = kDecodeStripeTiles;
   if (tiling == kDecodeStripeTiles) g.total_tiles = g.S * g.tiles_per_block;
-  if (tiling == kDecodeListTiles || tiling == kDecodeArgListTiles)
+  if (tiling == kDecodeListTiles || tiling == kDecodeArgListTiles ||
+      tiling == kDecodeDevListTiles)
     g.total_tiles = n_items * g.tiles_per_block;
   if (g.total_tiles == 0) return hipSuccess;
   ArgItems args;
@@ -499,6 +622,14 @@ hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_s
                         hipStream_t s) {
   const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
   check_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_list(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
+                            uint32_t* d_list, hipStream_t s) {
+  reset_status_list_kernel<<<1, 64, 0, s>>>(d_status, d_list);
+  const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
+  scan_list_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status, d_list);
   return hipGetLastError();
 }
 

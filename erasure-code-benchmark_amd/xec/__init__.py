@@ -6,7 +6,8 @@ multi-GPU partitioning helpers; it never computes parity itself.
 """
 from ._lib import EXPORTED, LIB_PATH, Status, XecLibraryError, lib
 from .codec import (DECODE_KERNELS, Pipeline, build_info, check_args, check_bitmap, decode,
-                    decode_device, decode_per_stripe, decode_tiling_used, encode, erase,
+                    decode_device, decode_device_list, decode_per_stripe, decode_tiling_used,
+                    device_list_bytes, encode, erase,
                     fill_splitmix64, init,
                     set_decode_tiling, set_launch, set_occupancy, set_validate_kernel,
                     status_string, validate_blocks, write_validation_pattern)
@@ -14,8 +15,8 @@ from .partition import stripe_range
 
 __all__ = [
     "DECODE_KERNELS", "EXPORTED", "LIB_PATH", "Pipeline", "Status", "XecLibraryError", "lib",
-    "build_info", "check_args", "check_bitmap", "decode", "decode_device", "decode_per_stripe",
-    "decode_tiling_used",
+    "build_info", "check_args", "check_bitmap", "decode", "decode_device", "decode_device_list",
+    "decode_per_stripe", "decode_tiling_used", "device_list_bytes",
     "encode", "erase", "fill_splitmix64", "init", "set_decode_tiling", "set_launch",
     "set_occupancy", "set_validate_kernel", "status_string", "stripe_range", "validate_blocks",
     "write_validation_pattern",

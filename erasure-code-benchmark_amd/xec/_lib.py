@@ -27,6 +27,7 @@ EXPORTED = (
     "xec_pipeline_decode", "xec_write_validation_pattern", "xec_validate_blocks",
     "xec_decode_device", "xec_set_occupancy", "xec_set_decode_tiling",
     "xec_set_validate_kernel", "xec_decode_tiling_used", "xec_decode_per_stripe",
+    "xec_decode_device_list", "xec_decode_device_list_bytes",
 )
 
 
@@ -93,6 +94,8 @@ def lib() -> ctypes.CDLL:
         "xec_write_validation_pattern": ([vp, sz, sz, ctypes.c_uint64, vp], st),
         "xec_validate_blocks": ([vp, sz, sz, vp, vp], st),
         "xec_decode_device": ([vp, vp, sz, sz, sz, sz, vp, vp, vp], st),
+        "xec_decode_device_list": ([vp, vp, sz, sz, sz, sz, vp, vp, sz, vp, vp], st),
+        "xec_decode_device_list_bytes": ([sz, sz, sz], sz),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

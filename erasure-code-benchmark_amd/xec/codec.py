@@ -67,6 +67,21 @@ def decode_device(d_data, d_parity, S: int, bs: int, k: int, m: int, d_bitmap, d
                                           _ptr(d_bitmap), _ptr(d_status), _stream(stream)))
 
 
+def decode_device_list(d_data, d_parity, S: int, bs: int, k: int, m: int, d_bitmap, d_work,
+                       work_bytes: int, d_status, stream=None) -> Status:
+    """xec_decode_device_list -- as decode_device, but the check kernel lists the
+    lost data blocks into d_work (device scratch of device_list_bytes(S, k, m)
+    bytes) and only those are rebuilt: for batches where few stripes lost blocks."""
+    return Status(lib().xec_decode_device_list(_ptr(d_data), _ptr(d_parity), S, bs, k, m,
+                                               _ptr(d_bitmap), _ptr(d_work), work_bytes,
+                                               _ptr(d_status), _stream(stream)))
+
+
+def device_list_bytes(S: int, k: int, m: int) -> int:
+    """xec_decode_device_list_bytes: scratch decode_device_list needs."""
+    return int(lib().xec_decode_device_list_bytes(S, k, m))
+
+
 def erase(d_data, d_parity, S: int, bs: int, k: int, m: int, d_bitmap, stream=None) -> Status:
     """xec_erase -- device-side simulate_data_loss (abstract_bm.cpp:20-39)."""
     return Status(lib().xec_erase(_ptr(d_data), _ptr(d_parity), S, bs, k, m, _ptr(d_bitmap),

@@ -123,6 +123,30 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
                              size_t m, const uint8_t* d_bitmap, int32_t* d_status,
                              hipStream_t stream);
 
+/* Device-resident decode for batches where only some stripes lost blocks (no
+ * reference counterpart; the device analogue of xec_decode's work-list tiles).
+ * xec_decode_device launches a tile for every (stripe, 1 KiB chunk) of the
+ * batch, so a batch where few stripes lost anything spends most of its
+ * workgroups finding nothing to do.  Here the check kernel also lists the
+ * lost data blocks into d_work (4-byte aligned device scratch of at least
+ * xec_decode_device_list_bytes(S, k, m) bytes, owned by the caller), and the
+ * decode is one tile per (listed block, chunk), handed out in order from
+ * work-queue heads in the scratch to a fixed grid of about what the chip holds
+ * at once (xec_set_launch's max_grid overrides it), since the host never sees
+ * the count.  Everything else as xec_decode_device: no
+ * host work (hipGraph-capturable), *d_status = 0 or 4 in stream order,
+ * all-or-nothing, parity read-only, identical bytes.  Requires k <= 256 and
+ * S <= 2^24 (else XEC_INVALID_SIZE), as does a too small work_bytes or a null
+ * d_bitmap with S > 0; d_status or d_work null or not 4-B aligned ->
+ * XEC_INVALID_ALIGNMENT; nothing is queued when an argument is rejected. */
+xec_status xec_decode_device_list(void* d_data, const void* d_parity, size_t S, size_t bs,
+                                  size_t k, size_t m, const uint8_t* d_bitmap, void* d_work,
+                                  size_t work_bytes, int32_t* d_status, hipStream_t stream);
+
+/* Scratch bytes xec_decode_device_list needs: a header (entry count and
+ * work-queue heads) and at most one 4-byte entry per parity class. */
+size_t xec_decode_device_list_bytes(size_t S, size_t k, size_t m);
+
 /* Host-only recoverability scan used by xec_decode (no GPU needed):
  * returns XEC_DECODE_FAILURE if some stripe is unrecoverable, else
  * XEC_SUCCESS and sets *needs_recovery to 1 iff some stripe needs recovery. */

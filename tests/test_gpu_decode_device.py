@@ -23,27 +23,47 @@ def _torch():
     return torch
 
 
-def _device_decode(xec, b, bm: np.ndarray, status_init: int = 0x7F):
-    """erase per bm, then xec_decode_device; returns (verdict, data, parity, erased data)."""
+def _decode_dev(xec, api, d, p, S, bs, k, m, d_bm, d_status, stream, work=None):
+    """One device-resident decode through `api`: "device" = xec_decode_device,
+    "list" = xec_decode_device_list (scratch `work`, allocated when None)."""
+    if api == "device":
+        return xec.decode_device(d, p, S, bs, k, m, d_bm, d_status, stream)
+    if work is None:
+        work = _torch().full((xec.device_list_bytes(S, k, m) // 4,), -1, dtype=torch_int32(),
+                             device="cuda")
+    return xec.decode_device_list(d, p, S, bs, k, m, d_bm, work, work.numel() * 4, d_status,
+                                  stream)
+
+
+def torch_int32():
+    return _torch().int32
+
+
+APIS = ["device", "list"]
+
+
+def _device_decode(xec, b, bm: np.ndarray, status_init: int = 0x7F, api: str = "device"):
+    """erase per bm, then xec_decode_device (or _list); returns (verdict, data, erased data)."""
     torch = _torch()
     d_bm = torch.from_numpy(np.ascontiguousarray(bm)).to("cuda")
     d_status = torch.full((1,), status_init, dtype=torch.int32, device="cuda")
     assert xec.erase(b.d, b.p, b.S, b.bs, b.k, b.m, d_bm, b.stream) == 0
     erased = b.data()
     erased_p = b.parity()
-    assert xec.decode_device(b.d, b.p, b.S, b.bs, b.k, b.m, d_bm, d_status, b.stream) == 0
+    assert _decode_dev(xec, api, b.d, b.p, b.S, b.bs, b.k, b.m, d_bm, d_status, b.stream) == 0
     torch.cuda.synchronize()
     got_p = b.parity()
     assert np.array_equal(got_p, erased_p), "decode_device wrote parity"
     return int(d_status.item()), b.data(), erased
 
 
-def test_golden_decode_fixtures_device(gpu, oracle, known_answers):
+@pytest.mark.parametrize("api", APIS)
+def test_golden_decode_fixtures_device(gpu, oracle, known_answers, api):
     for e in known_answers["decode"]:
         k, m, bs, S = e["k"], e["m"], e["bs"], e["S"]
         bm = np.fromfile(GOLDEN / "patterns" / e["pattern"], dtype=np.uint8)
         b, ref_d, _ = encode_and_check(gpu, oracle, S, k, m, bs, known_answers["seed"])
-        verdict, got, erased = _device_decode(gpu, b, bm)
+        verdict, got, erased = _device_decode(gpu, b, bm, api=api)
         if "4" in e["codes"]:
             assert verdict == gpu.Status.DECODE_FAILURE, e
             assert np.array_equal(got, erased), "failed batch was modified"
@@ -53,8 +73,9 @@ def test_golden_decode_fixtures_device(gpu, oracle, known_answers):
             assert f"{oracle.fnv1a64(got):016x}" == e["data_fnv_after"]
 
 
+@pytest.mark.parametrize("api", APIS)
 @pytest.mark.parametrize("k,m", [(4, 1), (16, 1), (8, 4), (12, 3), (40, 8), (6, 6), (66, 2)])
-def test_random_patterns_match_oracle_and_host_decode(gpu, oracle, k, m):
+def test_random_patterns_match_oracle_and_host_decode(gpu, oracle, k, m, api):
     """Same verdict and bytes as the oracle's all-or-nothing batch decode and as
     xec_decode (host scan), on random loss patterns including unrecoverable
     ones and bitmap bytes that are neither 0 nor 1."""
@@ -88,14 +109,15 @@ def test_random_patterns_match_oracle_and_host_decode(gpu, oracle, k, m):
         assert gpu.erase(host.d, host.p, S, bs, k, m, d_bm, host.stream) == 0
         st_host = gpu.decode(host.d, host.p, S, bs, k, m, h_bm, torch.empty_like(d_bm),
                              host.stream)
-        verdict, got, _ = _device_decode(gpu, dev, bm)
+        verdict, got, _ = _device_decode(gpu, dev, bm, api=api)
         assert verdict == want == int(st_host), (k, m, S, rows)
         assert np.array_equal(got, od), (k, m, S, rows)
         assert np.array_equal(host.data(), od)
         assert np.array_equal(dev.parity(), op)
 
 
-def test_full_size_cfg3_device(gpu):
+@pytest.mark.parametrize("api", APIS)
+def test_full_size_cfg3_device(gpu, api):
     """BASELINE configs[2] at full size (4 GiB): rebuilt data == a fresh fill."""
     torch = _torch()
     S, k, m, bs = 256, 16, 1, 1 << 20
@@ -105,7 +127,7 @@ def test_full_size_cfg3_device(gpu):
     d_bm = torch.from_numpy(bm).to("cuda")
     d_status = torch.full((1,), -1, dtype=torch.int32, device="cuda")
     assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == 0
-    assert gpu.decode_device(b.d, b.p, S, bs, k, m, d_bm, d_status, b.stream) == 0
+    assert _decode_dev(gpu, api, b.d, b.p, S, bs, k, m, d_bm, d_status, b.stream) == 0
     fresh = torch.empty_like(b.d)
     assert gpu.fill_splitmix64(fresh, S, k * bs, xo.RANDOM_SEED, b.stream) == 0
     torch.cuda.synchronize()
@@ -113,7 +135,8 @@ def test_full_size_cfg3_device(gpu):
     assert torch.equal(fresh, b.d)
 
 
-def test_graph_capture_encode_erase_decode(gpu, oracle):
+@pytest.mark.parametrize("api", APIS)
+def test_graph_capture_encode_erase_decode(gpu, oracle, api):
     """The device-resident path has no host work, so one hipGraph can hold
     encode -> erase -> decode; replays are bit-exact against the oracle."""
     torch = _torch()
@@ -125,6 +148,8 @@ def test_graph_capture_encode_erase_decode(gpu, oracle):
         oracle.select_lost_blocks(k, m, m, bm[c], 77 + c)
     d_bm = torch.from_numpy(bm.reshape(-1)).to("cuda")
     d_status = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    work = torch.full((gpu.device_list_bytes(S, k, m) // 4,), -1, dtype=torch.int32,
+                      device="cuda")
     torch.cuda.synchronize()
     side = torch.cuda.Stream()
     g = torch.cuda.CUDAGraph()
@@ -132,7 +157,7 @@ def test_graph_capture_encode_erase_decode(gpu, oracle):
         s = torch.cuda.current_stream()
         assert gpu.encode(b.d, b.p, S, bs, k, m, s) == 0
         assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, s) == 0
-        assert gpu.decode_device(b.d, b.p, S, bs, k, m, d_bm, d_status, s) == 0
+        assert _decode_dev(gpu, api, b.d, b.p, S, bs, k, m, d_bm, d_status, s, work) == 0
     for _ in range(2):
         d_status.fill_(-1)
         b.d[: S * k * bs].copy_(torch.from_numpy(ref_d).to("cuda"))
@@ -169,3 +194,92 @@ def test_device_argument_errors_and_empty_batch(gpu):
     torch.cuda.synchronize()
     assert st.tolist() == [0, 9, 9, 9]
     assert int(d.sum()) == 0 and int(p.sum()) == 0
+
+
+@pytest.mark.parametrize("k,m,bs,S,every", [(16, 1, 1 << 16, 512, 9), (8, 4, 4096, 3000, 5),
+                                            (32, 8, 1024, 777, 1), (40, 8, 768, 300, 3)])
+@pytest.mark.parametrize("max_grid", [0, 3])
+def test_device_list_sparse_patterns(gpu, k, m, bs, S, every, max_grid):
+    """Only every `every`-th stripe loses blocks (1..m per stripe, one per class):
+    xec_decode_device_list rebuilds exactly those, bit-exact against a fresh
+    fill, with the default grid and with a 3-workgroup grid that has to walk
+    the whole list (xec_set_launch max_grid)."""
+    import bench
+    torch = _torch()
+    rng = np.random.default_rng(S + every)
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(0, S, every):
+        lost = int(rng.integers(1, m + 1))
+        bm[c:c + 1] = bench.erasure_pattern(np, 1, k, m, lost, start=c)
+    b = Batch(gpu, S, k, m, bs, seed=33)
+    assert gpu.encode(b.d, b.p, S, bs, k, m, b.stream) == 0
+    fresh = b.data()
+    assert gpu.set_launch(0, max_grid, 0, 0) == 0
+    try:
+        verdict, got, erased = _device_decode(gpu, b, bm.reshape(-1), api="list")
+    finally:
+        assert gpu.set_launch(0, 0, 0, 0) == 0
+    assert verdict == 0
+    assert not np.array_equal(erased, fresh)
+    assert np.array_equal(got, fresh)
+
+
+def test_device_list_writes_one_entry_per_lost_block(gpu):
+    """The scratch after a call: count = lost data blocks, entries (after the
+    header) = their (c << 8 | i) items in some order, nothing past them."""
+    torch = _torch()
+    S, k, m, bs = 100, 12, 4, 256
+    rng = np.random.default_rng(5)
+    bm = np.ones((S, k + m), np.uint8)
+    want = set()
+    for c in range(S):
+        for j in range(m):
+            if rng.random() < 0.3:
+                i = j + m * int(rng.integers(0, k // m))
+                bm[c, i] = 0
+                want.add(c << 8 | i)
+        if rng.random() < 0.2:
+            bm[c, k + int(rng.integers(0, m))] = 0  # lost parity of a class: listed only if
+    for c in range(S):                              # that class lost no data block
+        for j in range(m):
+            if bm[c, k + j] == 0 and any(bm[c, j::m][:k // m] == 0):
+                bm[c, k + j] = 1
+    b = Batch(gpu, S, k, m, bs)
+    d_bm = torch.from_numpy(bm.reshape(-1)).to("cuda")
+    st = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    n = gpu.device_list_bytes(S, k, m) // 4
+    work = torch.full((n + 8,), -7, dtype=torch.int32, device="cuda")
+    assert gpu.decode_device_list(b.d, b.p, S, bs, k, m, d_bm, work, (n + 8) * 4, st) == 0
+    torch.cuda.synchronize()
+    w = work.cpu().numpy().view(np.uint32)
+    assert int(st.item()) == 0
+    assert w[0] == len(want)
+    hdr = n - S * m  # header words
+    assert set(int(x) for x in w[hdr:hdr + len(want)]) == want
+    assert (work.cpu().numpy()[hdr + len(want):] == -7).all()
+
+
+def test_device_list_argument_errors(gpu):
+    torch = _torch()
+    S_ = gpu.Status
+    d = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    p = torch.zeros(1 << 14, dtype=torch.uint8, device="cuda")
+    bm = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    st = torch.full((4,), 9, dtype=torch.int32, device="cuda")
+    w = torch.full((16,), 9, dtype=torch.int32, device="cuda")
+    need = gpu.device_list_bytes(2, 4, 2)
+    assert need == gpu.device_list_bytes(0, 4, 2) + 4 * 2 * 2
+    call = gpu.decode_device_list
+    assert call(d, p, 2, 4096, 4, 2, bm, w.data_ptr() + 2, need, st) == S_.INVALID_ALIGNMENT
+    assert call(d, p, 2, 4096, 4, 2, bm, 0, need, st) == S_.INVALID_ALIGNMENT
+    assert call(d, p, 2, 4096, 4, 2, bm, w, need, st.data_ptr() + 1) == S_.INVALID_ALIGNMENT
+    assert call(d, p, 2, 4096, 4, 2, bm, w, need - 4, st) == S_.INVALID_SIZE
+    assert call(d, p, 2, 4096, 4, 2, 0, w, need, st) == S_.INVALID_SIZE
+    assert call(d, p, 1, 256, 300, 1, bm, w, 64, st) == S_.INVALID_SIZE  # k > 256
+    assert call(d, p, 2, 100, 4, 2, bm, w, need, st) == S_.INVALID_SIZE
+    assert call(d, p, 2, 4096, 6, 4, bm, w, need, st) == S_.INVALID_COUNTS
+    torch.cuda.synchronize()
+    assert st.tolist() == [9] * 4 and w.tolist() == [9] * 16, "rejected calls enqueue nothing"
+    assert call(d, p, 0, 4096, 4, 2, 0, w, 0, st) == S_.SUCCESS  # S=0: verdict 0, no scratch use
+    torch.cuda.synchronize()
+    assert st.tolist() == [0, 9, 9, 9] and w.tolist() == [9] * 16

@@ -3,7 +3,8 @@
 
 For each shape and each number of lost data blocks per stripe (one per class,
 bench.erasure_pattern), times xec_decode with stripe tiles (1), class tiles (2),
-work-list tiles (3) and the automatic choice (0) in interleaved rounds on the
+work-list tiles (3) and the automatic choice (0) -- with --device also
+xec_decode_device and xec_decode_device_list -- in interleaved rounds on the
 same buffers (three
 rotating buffer sets, HIP events on the launching stream), and checks every
 variant rebuilt the erased blocks bit-exactly (against a fresh device fill).
@@ -45,6 +46,9 @@ def main():
                     help="time class tiles (and their --occ variants) and encode only")
     ap.add_argument("--pattern", default="uniform", choices=["uniform", "sparse", "skew"])
     ap.add_argument("--variants", default="", help="comma list to keep (e.g. class,list)")
+    ap.add_argument("--device", action="store_true",
+                    help="also time the device-resident decodes: xec_decode_device (dev) and "
+                         "xec_decode_device_list (devlist), bitmap already in HBM")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -88,6 +92,21 @@ def main():
                 variants = {"class": (2, None)}
             for o in (int(x) for x in args.occ.split(",") if x):
                 variants[f"class@o{o}"] = (2 if m > 1 else 1, o)
+            if args.device:
+                variants["dev"] = (0, None)
+                variants["devlist"] = (0, None)
+            d_status = torch.zeros((1,), dtype=torch.int32, device="cuda")
+            wbytes = xec.device_list_bytes(S, k, m)
+            work = torch.empty((wbytes // 4,), dtype=torch.int32, device="cuda")
+
+            def run_decode(v, d, p, scr):
+                if v == "dev":
+                    return xec.decode_device(d, p, S, bs, k, m, d_bm, d_status, stream)
+                if v == "devlist":
+                    return xec.decode_device_list(d, p, S, bs, k, m, d_bm, work, wbytes,
+                                                  d_status, stream)
+                return xec.decode(d, p, S, bs, k, m, h_bm, scr, stream)
+
             if args.variants:
                 keep = set(args.variants.split(","))
                 variants = {v: t for v, t in variants.items() if v in keep}
@@ -110,7 +129,7 @@ def main():
                         if v == "encode":
                             assert xec.encode(d, p, S, bs, k, m, stream) == 0
                         else:
-                            assert xec.decode(d, p, S, bs, k, m, h_bm, scratch[it % 3], stream) == 0
+                            assert run_decode(v, d, p, scratch[it % 3]) == 0
                         evs[i][1].record(stream)
                     torch.cuda.synchronize()
                     times[v] += [a.elapsed_time(b) for a, b in evs]
@@ -122,9 +141,9 @@ def main():
                 assert xec.set_occupancy(t[1] or 0) == 0
                 d, p = sets[0]
                 assert xec.erase(d, p, S, bs, k, m, d_bm, stream) == 0
-                assert xec.decode(d, p, S, bs, k, m, h_bm, scratch[0], stream) == 0
+                assert run_decode(v, d, p, scratch[0]) == 0
                 assert xec.fill_splitmix64(fresh, S, k * bs, 1000, stream) == 0
-                ok[v] = bool(torch.equal(fresh, d))
+                ok[v] = bool(torch.equal(fresh, d)) and int(d_status.item()) == 0
             assert xec.set_decode_tiling(0) == 0
             assert xec.set_occupancy(0) == 0
             del fresh
