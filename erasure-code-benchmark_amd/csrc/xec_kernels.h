@@ -65,15 +65,11 @@ constexpr int kDecodeClassTiles = 1;
 constexpr int kDecodeListTiles = 2;
 constexpr int kDecodeArgListTiles = 3;
 // DevList: list tiles over a list the device built (launch_scan_list):
-// d_bitmap = the u32 list: [0] = entry count, work-queue head h at
-// [kDevListHeadStride * (1 + h)], entries from [kDevListHeader]; n_items = the
-// most entries there can be (sizes the grid with ls.max_grid; g.gate must be
-// set).
+// d_bitmap = the u32 list, [0] = entry count, entries from [kDevListHeader];
+// n_items = the most entries there can be (sizes the grid with ls.max_grid;
+// g.gate must be set).
 constexpr int kDecodeDevListTiles = 4;
-constexpr uint32_t kDevListHeads = 8;        // one per XCD
-constexpr uint32_t kDevListHeadStride = 64;  // u32 words between heads (256 B)
-constexpr uint32_t kDevListGrab = 4;         // consecutive tiles of a head per pull
-constexpr uint32_t kDevListHeader = kDevListHeadStride * (kDevListHeads + 1);
+constexpr uint32_t kDevListHeader = 1;  // u32 words before the first entry
 constexpr uint64_t kArgItems = 1024;
 struct ArgItems {
   uint32_t v[kArgItems];

@@ -321,70 +321,27 @@ __global__ __launch_bounds__(T) void decode_arglist_kernel(uint8_t* data,
   }
 }
 
-// The same with a list the device built (xec_decode_device_list; layout in
-// xec_kernels.h kDevListHeader): the entry count is what scan_list_kernel
-// left, so the host cannot size the grid to it.  The launch is a fixed grid
-// of about what the chip holds at once, and the tiles are handed out in
-// order from work-queue heads rather than by a grid-stride walk: a
-// grid-stride walk lets each workgroup run at its own pace, so after a while
-// the tiles in flight spread over many stripes, which measured 10-18 % slower
-// than one workgroup per tile on dense batches (profiles/r02af).  With
-// H = min(8, grid) heads, workgroup b pulls from head h = b % H (round-robin
-// dispatch puts h on XCD h, so one head serves one XCD: one head word
-// saturates at ~88 dequeues/us, MI355X_MICROARCH.md, dequeue), and the q-th
-// pull of head h is tile q*H + h -- the tile one-workgroup-per-tile dispatch
-// would give that XCD next.  The next pull is issued before the current tile's
-// loads, so its latency hides behind them.  Every workgroup leaves once its
-// head runs past the count, which every head does.
-// A pull is issued by lane 0 (its value lives in lane 0 only) and handed to
-// the workgroup later, after the tile's loads and store have been issued;
-// the scheduling barriers keep the compiler from waiting on the atomic (and
-// so on the fabric round trip) before the tile's loads leave.
-__device__ __forceinline__ uint32_t devlist_issue(uint32_t* head) {
-  uint32_t q = 0;
-  // inc (wrapping at 2^32 - 1, i.e. +1 here), not add: the compiler's atomic
-  // optimizer rewrites a returning add into a wave-aggregated one whose
-  // per-lane result it computes, i.e. waits for, right away
-  if (threadIdx.x == 0) q = atomicInc(head, 0xFFFFFFFFu);
-  return q;
-}
-
-template <int T>
-__device__ __forceinline__ uint32_t devlist_bcast(uint32_t q) {
-  if constexpr (T == 64) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)q);
-  } else {
-    __shared__ uint32_t sq;
-    __syncthreads();  // every wave has read the previous pull
-    if (threadIdx.x == 0) sq = q;
-    __syncthreads();
-    return sq;
-  }
-}
-
+// The same with a list the device built (xec_decode_device_list): list[0] is
+// the entry count scan_list_kernel left, entries from list[1].  The host
+// never sees the count, so the launch is a fixed grid of about what the chip
+// holds at once, walking the count's tiles in grid strides.  On sparse
+// batches that is 1.8-3.7x faster than decode_kernel over every stripe; on
+// dense ones 5-19 % slower than one workgroup per tile, and handing the tiles
+// out in order from per-XCD work-queue heads instead was no better (0-31 %
+// behind, commit 6f8fb1e, profiles/r02af, r02ag, r02ah), so the walk stays
+// simple.  The gate is the check's verdict, as in decode_kernel.
 template <int NM, int U, bool NT, int T>
 __global__ __launch_bounds__(T) void decode_devlist_kernel(uint8_t* data,
                                                            const uint8_t* __restrict__ parity,
-                                                           uint32_t* list, Geometry g) {
+                                                           const uint32_t* __restrict__ list,
+                                                           Geometry g) {
   if (*(const_i32_as4)g.gate != 0) return;
   const uint64_t total = (uint64_t)*(const_u32_as4)list * g.tiles_per_block;
-  const uint32_t nh = gridDim.x < kDevListHeads ? gridDim.x : kDevListHeads;
-  const uint32_t h = blockIdx.x % nh;
-  uint32_t* head = list + kDevListHeadStride * (1 + h);
   const uint32_t* entries = list + kDevListHeader;
-  uint64_t q = devlist_bcast<T>(devlist_issue(head));
-  while ((q * kDevListGrab) * nh + h < total) {
-    const uint32_t qn = devlist_issue(head);
-    __builtin_amdgcn_sched_barrier(0);
-    for (uint32_t i = 0; i < kDevListGrab; ++i) {
-      const uint64_t t0 = (q * kDevListGrab + i) * nh + h;
-      if (t0 >= total) break;
-      const uint64_t t = total - 1 - t0;  // from the end of the list, as the other kernels
-      const uint32_t item = *(const_u32_as4)(entries + t / g.tiles_per_block);
-      rebuild_item<NM, U, NT, T>(data, parity, item, t % g.tiles_per_block, g);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    q = devlist_bcast<T>(qn);
+  for (uint64_t t0 = blockIdx.x; t0 < total; t0 += gridDim.x) {
+    const uint64_t t = total - 1 - t0;  // from the end of the list, as the other kernels
+    const uint32_t item = *(const_u32_as4)(entries + t / g.tiles_per_block);
+    rebuild_item<NM, U, NT, T>(data, parity, item, t % g.tiles_per_block, g);
   }
 }
 
@@ -430,11 +387,11 @@ __global__ __launch_bounds__(256) void scan_list_kernel(const uint8_t* __restric
   }
 }
 
-// *status = 0 and the list header (count, work-queue heads) = 0 in one launch,
-// stream-ordered before the scan.
+// *status = 0 and the list's count = 0 in one launch, stream-ordered before
+// the scan.
 __global__ void reset_status_list_kernel(int32_t* status, uint32_t* list) {
-  if (threadIdx.x == 0) *status = 0;
-  if (threadIdx.x <= kDevListHeads) list[kDevListHeadStride * threadIdx.x] = 0u;  // count, heads
+  *status = 0;
+  *list = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -512,7 +469,7 @@ hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geom
   if (tiling == kDecodeDevListTiles)
     decode_devlist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
         static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p),
-        reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(bm)), g);
+        reinterpret_cast<const uint32_t*>(bm), g);
   else if (tiling == kDecodeArgListTiles)
     decode_arglist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
         static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p), g, *args);
@@ -627,7 +584,7 @@ hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_s
 
 hipError_t launch_scan_list(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
                             uint32_t* d_list, hipStream_t s) {
-  reset_status_list_kernel<<<1, 64, 0, s>>>(d_status, d_list);
+  reset_status_list_kernel<<<1, 1, 0, s>>>(d_status, d_list);
   const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
   scan_list_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status, d_list);
   return hipGetLastError();
