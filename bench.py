@@ -70,7 +70,8 @@ def parse():
                     help="nccl = RCCL (default); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--no-scatter", action="store_true",
                     help="skip the N>1 scatter-inclusive measurement (RCCL send/recv)")
-    ap.add_argument("--scatter-timeout", type=float, default=120.0)
+    ap.add_argument("--scatter-timeout", type=float, default=120.0,
+                    help="watchdog (s) over the legs after the headline: host pipeline, scatter")
     ap.add_argument("--lost", type=int, default=1,
                     help="lost data blocks per stripe (1..m, one per parity class); the "
                          "BASELINE workloads lose one")
@@ -89,6 +90,10 @@ def parse():
     ap.add_argument("--rehearse-cpu", action="store_true",
                     help="CPU stand-ins for every device call (tools/cpu_rehearsal.py), gloo "
                          "only: rehearses the launcher and N>1 bookkeeping; measures nothing")
+    ap.add_argument("--no-host-pipeline", action="store_true",
+                    help="skip the host-in/host-out leg (xec_pipeline, pinned host memory)")
+    ap.add_argument("--host-stripes", type=int, default=0,
+                    help="stripes per rank for the host-in/host-out leg (0 = 1 GiB of data)")
     ap.add_argument("--rank-grace", type=float, default=60.0,
                     help="launcher: seconds to wait for the other ranks after one fails")
     return ap.parse_args()
@@ -313,6 +318,77 @@ def measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms, reps=
             "gathered_parity_bit_exact_vs_root_encode": ok_ga,
             "note": f"batch starts on rank 0; {dist.get_backend()} send/recv of stripe ranges "
                     "(RCCL over xGMI with nccl); link-bound"}
+
+
+HOST_CHUNK_STRIPES, HOST_STREAMS = 8, 3  # best measured pipeline shape
+
+
+def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3):
+    """North star's end-to-end rate: each rank
+    streams a batch that starts and ends in its own pinned host memory through
+    its GPU with xec_pipeline (H2D -> kernel -> D2H, chunks over streams), all
+    ranks at once between barriers.  Encode returns the parity to the host;
+    decode rebuilds one lost data block per stripe in host memory.  Returns this
+    rank's (encode s, decode s, bit-exact, error); every rank makes the same
+    collective calls whatever fails locally.  PCIe-bound: reported beside, never
+    as, the device-resident value."""
+    import numpy as np
+    use_dist = dist.is_initialized()
+
+    def agree(flag):
+        if not use_dist:
+            return flag
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return t.item() == 1.0
+
+    err = None
+    try:  # setup: pinned host batch, its parity and an erasure pattern
+        h_d = torch.empty(S * k * bs, dtype=torch.uint8).pin_memory()
+        h_p = torch.empty(S * m * bs, dtype=torch.uint8).pin_memory()
+        d_d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+        d_p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+        st = torch.cuda.current_stream()
+        assert xec.fill_splitmix64(d_d, S, k * bs, SEED + start, st) == 0
+        assert xec.encode(d_d, d_p, S, bs, k, m, st) == 0
+        h_d.copy_(d_d)
+        ref_p = d_p.cpu()
+        ref_d = h_d.clone()
+        del d_d, d_p
+        bm = erasure_pattern(np, S, k, m, 1, start)
+        h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
+        hv = h_d.numpy().reshape(S, k, bs)
+        pl = xec.Pipeline(HOST_CHUNK_STRIPES, bs, k, m, HOST_STREAMS)
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        err = repr(e)[:200]
+    if not agree(err is None):
+        return 0.0, 0.0, False, err or "another rank failed its setup"
+
+    rcs = []
+
+    def timed(fn, before=None):
+        ts = []
+        for _ in range(reps + 1):  # the first is a warm-up
+            if before is not None:
+                before()
+            if use_dist:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rcs.append(int(fn()))
+            ts.append(time.perf_counter() - t0)
+        return min(ts[1:])
+
+    def erase():
+        hv[bm[:, :k] == 0] = 0
+
+    h_p.zero_()
+    t_enc = timed(lambda: pl.encode(h_d, h_p, S))
+    ok = bool(torch.equal(h_p, ref_p))
+    t_dec = timed(lambda: pl.decode(h_d, h_p, S, h_bm), before=erase)
+    ok &= bool(torch.equal(h_d, ref_d)) and not any(rcs)
+    pl.close()
+    return t_enc, t_dec, ok, (f"xec_pipeline status {sorted(set(rcs))}" if any(rcs) else None)
 
 
 def launch_ranks(n, argv, grace_s):
@@ -660,18 +736,25 @@ def run_rank(args):
     else:
         out = None
 
-    # Config 5's scatter leg runs after the headline numbers are final, under a
-    # watchdog: a stuck link can cost this extra field, never the result line.
-    # On expiry every rank exits 3; the bench.py launcher reads 3 as "headline
-    # printed, scatter leg hung" (scatter.error is authoritative), an external
-    # launcher sees the non-zero status.
-    # (gloo cannot carry HIP buffers: with --dist-backend gloo on a GPU the leg is skipped)
-    if use_dist and not args.no_scatter and not bad and (backend == "nccl" or args.rehearse_cpu):
+    # Two legs run after the headline numbers are final, under one watchdog: a
+    # stuck link or copy can cost their fields, never the result line.  On
+    # expiry every rank exits 3 (rank 0 prints the line first); the bench.py
+    # launcher reads 3 as "headline printed, an extra leg hung" (the leg's
+    # "error" is authoritative), an external launcher sees the non-zero status.
+    #  * host_pipeline: the north star's host-in / host-out rate, every rank;
+    #  * scatter: config 5's RCCL scatter / gather (N > 1; gloo cannot carry
+    #    HIP buffers, so with --dist-backend gloo on a GPU it is skipped).
+    host_leg = not args.no_host_pipeline and not args.rehearse_cpu and args.lost == 1 and not bad
+    scatter_leg = (use_dist and not args.no_scatter and not bad
+                   and (backend == "nccl" or args.rehearse_cpu))
+    if host_leg or scatter_leg:
         import threading
 
         def on_timeout():
             if out is not None:
-                out["scatter"] = {"error": f"timed out after {args.scatter_timeout:.0f} s"}
+                for leg, on in (("host_pipeline", host_leg), ("scatter", scatter_leg)):
+                    if on and leg not in out:
+                        out[leg] = {"error": f"timed out ({args.scatter_timeout:.0f} s watchdog)"}
                 print(json.dumps(out), flush=True)
             sys.stderr.flush()
             os._exit(3)
@@ -679,15 +762,48 @@ def run_rank(args):
         dog = threading.Timer(args.scatter_timeout, on_timeout)
         dog.daemon = True
         dog.start()
-        try:
-            ops = DeviceOps(torch, xec, stream, k, m, bs)
-            ops.device, ops.sync = coll_dev, cuda.synchronize
-            sc = measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms)
-        except Exception as e:  # noqa: BLE001 - report, keep the headline line
-            sc = {"error": repr(e)[:200]}
+        if host_leg:
+            hs = args.host_stripes or max(1, (1 << 30) // (k * bs))
+            t_enc, t_dec, ok_h, err = measure_host_pipeline(torch, dist, xec, k, m, bs, hs, start,
+                                                            coll_dev)
+            mine = torch.tensor([t_enc, t_dec, 1.0 if ok_h else 0.0], dtype=torch.float64,
+                                device=coll_dev)
+            if use_dist:
+                hrows = [torch.zeros_like(mine) for _ in range(world)]
+                dist.all_gather(hrows, mine)
+                hrows = [r.tolist() for r in hrows]
+            else:
+                hrows = [mine.tolist()]
+            if out is not None:
+                te, td = max(r[0] for r in hrows), max(r[1] for r in hrows)
+                data_all = world * hs * k * bs
+                hp = {"encode_GBps_data": round(data_all / te / 1e9, 2) if te > 0 else None,
+                      "decode_GBps_data": round(data_all / td / 1e9, 2) if td > 0 else None,
+                      "bit_exact": all(r[2] == 1.0 for r in hrows),
+                      "per_rank_encode_GBps_data": [
+                          round(hs * k * bs / r[0] / 1e9, 2) if r[0] else None for r in hrows],
+                      "sample": f"{hs} stripes ({hs * k * bs >> 20} MiB data) per rank in pinned "
+                                f"host memory, xec_pipeline {HOST_CHUNK_STRIPES}-stripe chunks x "
+                                f"{HOST_STREAMS} streams, all ranks at once, best of 3 after a "
+                                "warm-up, max over ranks; encode = data in, parity out; decode "
+                                "= survivors in, one rebuilt block per stripe out",
+                      "note": "end-to-end, PCIe-bound (DESIGN.md §7); reported beside the "
+                              "device-resident value, never as it"}
+                if err:
+                    hp["error"] = err
+                out["host_pipeline"] = hp
+            if err:
+                print(f"rank {rank}: host_pipeline: {err}", file=sys.stderr)
+        if scatter_leg:
+            try:
+                ops = DeviceOps(torch, xec, stream, k, m, bs)
+                ops.device, ops.sync = coll_dev, cuda.synchronize
+                sc = measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms)
+            except Exception as e:  # noqa: BLE001 - report, keep the headline line
+                sc = {"error": repr(e)[:200]}
+            if out is not None:
+                out["scatter"] = sc
         dog.cancel()
-        if out is not None:
-            out["scatter"] = sc
     if out is not None:
         print(json.dumps(out), flush=True)
     if use_dist:

@@ -46,6 +46,9 @@ def test_bench_json_line(workload, stripes):
     assert c["by_workload"][workload]["value"] == c["value"]
     assert out["value"] > 0
     assert out["dist"]["ranks_seen"] == 1 and len(out["per_rank"]) == 1
+    hp = out["host_pipeline"]  # the north star's host-in / host-out leg
+    assert hp["bit_exact"] is True and "error" not in hp, hp
+    assert hp["encode_GBps_data"] > 0 and hp["decode_GBps_data"] > 0
 
 
 def test_bench_device_decode_api():
@@ -88,6 +91,7 @@ def test_bench_rccl_world1():
     sc = out["scatter"]
     assert sc.get("bit_exact") is True, sc
     assert sc["gathered_parity_bit_exact_vs_root_encode"] is True
+    assert out["host_pipeline"]["bit_exact"] is True
 
 
 def test_bench_launcher_two_ranks_one_gpu():
@@ -98,3 +102,5 @@ def test_bench_launcher_two_ranks_one_gpu():
     assert out["n_gpus"] == 2 and out["verified"] is True
     assert out["dist"] == {"backend": "gloo", "ranks_seen": 2, "launcher": "bench.py"}
     assert out["config"]["stripes_total"] == 64 and len(out["per_rank"]) == 2
+    hp = out["host_pipeline"]  # both ranks stream their own host batch at once
+    assert hp["bit_exact"] is True and len(hp["per_rank_encode_GBps_data"]) == 2, hp
