@@ -70,3 +70,93 @@ def test_block_larger_than_2gib(gpu):
     assert gpu.decode(d, p, S, bs, k, m, h_bm, torch.empty_like(d_bm), s) == gpu.Status.SUCCESS
     torch.cuda.synchronize()
     assert torch.equal(d[bs:], keep)
+
+
+DECODE_PATHS = ["auto", "stripe", "class", "list", "per_stripe", "device", "device_list"]
+
+
+def _recoverable_rows(bm, k, m):
+    """is_recoverable per stripe (xorec_utils.hpp:160-175): every class has at
+    most one lost block among its data members and its parity."""
+    lost = bm == 0
+    ok = np.ones(bm.shape[0], bool)
+    for j in range(m):
+        ok &= (lost[:, j:k:m].sum(axis=1) + lost[:, k + j]) <= 1
+    return ok
+
+
+def _decode_via(gpu, path, b, h_bm, d_bm):
+    """Run one decode entry point (or forced tiling); returns the status the
+    host sees (device paths: the device verdict)."""
+    import torch
+    S, k, m, bs = b.S, b.k, b.m, b.bs
+    if path in ("auto", "stripe", "class", "list"):
+        assert gpu.set_decode_tiling({"auto": 0, "stripe": 1, "class": 2, "list": 3}[path]) == 0
+        return int(gpu.decode(b.d, b.p, S, bs, k, m, h_bm, torch.empty_like(d_bm), b.stream))
+    if path == "per_stripe":
+        return int(gpu.decode_per_stripe(b.d, b.p, S, bs, k, m, h_bm, torch.empty_like(d_bm),
+                                         None, b.stream))
+    st = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    if path == "device":
+        assert gpu.decode_device(b.d, b.p, S, bs, k, m, d_bm, st, b.stream) == 0
+    else:
+        n = gpu.device_list_bytes(S, k, m)
+        w = torch.empty((n + 3) // 4, dtype=torch.int32, device="cuda")
+        rc = gpu.decode_device_list(b.d, b.p, S, bs, k, m, d_bm, w, n, st, b.stream)
+        if rc != 0:
+            return int(rc)
+    torch.cuda.synchronize()
+    return int(st.item())
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_random_shape_every_decode_path(gpu, oracle, case):
+    """Every decode entry point and forced tiling on the same random shape and
+    loss pattern, bit-exact against the oracle: the batch paths all-or-nothing
+    (xorec_gpu_cmp.cu:75-81), xec_decode_per_stripe stripe by stripe
+    (xorec_bm.cpp:43-58); parity never written.  k > 256 (the list's limit):
+    the list-only entry points must refuse with InvalidSize and touch nothing."""
+    import torch
+    rng = np.random.default_rng(777 + case)
+    S, k, m, bs = _random_case(rng)
+    S = max(S, 3)
+    S = min(S, max(1, (24 << 20) // (k * bs)))
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs, seed=1300 + case)
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(S):
+        oracle.select_lost_blocks(k, m, int(rng.integers(0, m + 1)), bm[c], 31 * case + c)
+    if case % 3 == 0:  # one unrecoverable stripe
+        c = int(rng.integers(0, S))
+        bm[c, :] = 1
+        bm[c, 0] = 0
+        bm[c, k] = 0
+    rec = _recoverable_rows(bm, k, m)
+    h_bm = torch.from_numpy(bm.reshape(-1).copy()).pin_memory()
+    d_bm = h_bm.to("cuda")
+    ref_dt = torch.from_numpy(ref_d).to("cuda")
+    want_p = ref_p.reshape(S, m, bs).copy()
+    want_p[bm[:, k:] == 0] = 0
+    try:
+        for path in DECODE_PATHS:
+            b.d[: S * k * bs].copy_(ref_dt)
+            assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == 0
+            erased = b.data().reshape(S, k, bs).copy()
+            st = _decode_via(gpu, path, b, h_bm, d_bm)
+            got = b.data().reshape(S, k, bs)
+            assert np.array_equal(b.parity().reshape(S, m, bs), want_p), (path, "parity written")
+            if k > 256 and path in ("per_stripe", "device_list"):
+                assert st == gpu.Status.INVALID_SIZE, path
+                assert np.array_equal(got, erased), path
+                continue
+            if path == "per_stripe":
+                want = np.where(rec[:, None, None], ref_d.reshape(S, k, bs), erased)
+                assert st == (0 if rec.all() else 4), path
+            elif rec.all():
+                want = ref_d.reshape(S, k, bs)
+                assert st == 0, path
+            else:
+                want = erased
+                assert st == 4, path
+            assert np.array_equal(got, want), (path, S, k, m, bs)
+    finally:
+        gpu.set_decode_tiling(0)
