@@ -49,6 +49,20 @@ xec_status sync_all(xec_pipeline* p) {
   return st;
 }
 
+// The pipeline's streams and slots belong to the device current at create;
+// each call runs there and gives the caller's current device back.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    ok = hipGetDevice(&prev) == hipSuccess && (prev == dev || hipSetDevice(dev) == hipSuccess);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (ok && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 // Error exit: drain what was already queued so no copy touches the caller's
 // buffers after the call returns.
 xec_status fail(xec_pipeline* p, xec_status st) {
@@ -112,6 +126,7 @@ xec_status xec_pipeline_create(xec_pipeline** out, size_t chunk_stripes, size_t 
 
 xec_status xec_pipeline_destroy(xec_pipeline* p) {
   if (!p) return XEC_SUCCESS;
+  const DeviceGuard dg(p->device);
   destroy_slots(p);
   delete p;
   return XEC_SUCCESS;
@@ -119,6 +134,8 @@ xec_status xec_pipeline_destroy(xec_pipeline* p) {
 
 xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_parity, size_t S) {
   if (!p) return XEC_NOT_INITIALIZED;
+  const DeviceGuard dg(p->device);
+  if (!dg.ok) return XEC_DEVICE_ERROR;
   const size_t k = p->k, m = p->m, bs = p->bs;
   const auto* src = static_cast<const uint8_t*>(h_data);
   auto* dst = static_cast<uint8_t*>(h_parity);
@@ -142,6 +159,8 @@ xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_pari
 xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_parity, size_t S,
                                const uint8_t* h_bitmap) {
   if (!p) return XEC_NOT_INITIALIZED;
+  const DeviceGuard dg(p->device);
+  if (!dg.ok) return XEC_DEVICE_ERROR;
   const size_t k = p->k, m = p->m, bs = p->bs, row = k + m;
   int needs = 0;
   xec_status st = xec_check_bitmap(h_bitmap, S, k, m, &needs);

@@ -35,6 +35,8 @@ struct BenchmarkConfig {
   int sync_mode = 0;            // new: 0 runtime default, 1 spin, 2 yield, 3 blocking sync
                                 // (hipSetDeviceFlags; CUDA's default "auto" spins when
                                 // contexts < cores, which is what the reference ran under)
+  std::vector<int> devices;     // new: XorecBenchmarkHipMulti's devices, one stripe range
+                                // each (repeats allowed); empty = every visible device
 };
 
 // The reference's sweep vectors (src/benchmark/bm_config.cpp:3-23,

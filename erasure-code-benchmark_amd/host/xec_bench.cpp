@@ -1,9 +1,12 @@
 // xec_bench.cpp -- command-line harness with the reference's CLI contract
-// (src/utils/benchmark_suite.cpp:102-212) for the HIP XOR-EC plugin,
-// registered as GPU algorithm "xorec-hip" beside the reference's "xorec-gpu"
+// (src/utils/benchmark_suite.cpp:102-212) for the HIP XOR-EC plugins,
+// registered as GPU algorithms "xorec-hip" (one device, XorecBenchmarkHip) and
+// "xorec-hip-multi" (the batch's stripes split over several devices of this
+// process, XorecBenchmarkHipMulti) beside the reference's "xorec-gpu"
 // (benchmark_suite.cpp:56-62; runners.cpp:43-45).
 //
-//   xec_bench -g xorec-hip [-f out.csv] [-a] [-i iters] [-w warmup] [-s simd,...] [-h]
+//   xec_bench -g xorec-hip[,xorec-hip-multi] [-f out.csv] [-a] [-i iters] [-w warmup]
+//             [-s simd,...] [-h]
 //
 //   -f, --file        output CSV (must contain ".csv"; default results.csv), written
 //                     at the given path (the reference prefixes ../results/raw/)
@@ -11,7 +14,7 @@
 //                     csv_reporter.cpp:11-19)
 //   -i, --iterations  timed iterations per config (> 0, default 10)
 //   -w, --warmup      warm-up iterations per config (>= 0, default 0)
-//   -g, --gpu         GPU algorithms, comma separated: xorec-hip
+//   -g, --gpu         GPU algorithms, comma separated: xorec-hip, xorec-hip-multi
 //   -c, --cpu         CPU algorithms are outside this build (error)
 //   -s, --simd        CPU XOR-EC SIMD versions (scalar, sse2, avx2, avx512): validated
 //                     like the reference; they select CPU variants only, so no effect here
@@ -19,14 +22,16 @@
 // product (get_gpu_configs, benchmark_suite.cpp:252-277, over the vectors of
 // bm_config.cpp:3-23): 8 MiB messages x block sizes x EC params x lost blocks
 // (<= m) x 256 GPU blocks x 512 threads, one 20-column CSV row each, in the
-// reference's order.
+// reference's order, algorithm by algorithm (get_benchmarks, :279-311).
 //
 // Extensions (long options only):
 //   --message B --block B --data K --parity M --lost L   one config instead of the sweep
 //                                    (sizes accept K/M/G suffixes, binary)
 //   --sweep FILE     configs from FILE, one "message block k m lost" per line
 //   --threads N      host threads for host-side validation (default: all)
-//   --device D       HIP device (default 0)
+//   --device D       HIP device of xorec-hip (default 0)
+//   --devices LIST   devices of xorec-hip-multi, comma separated, repeats allowed
+//                    (default: every visible device)
 //   --seed S         seed of payloads and erasure draws (the reference uses the clock)
 //   --sync MODE      hipSetDeviceFlags: 0 default, 1 spin, 2 yield, 3 blocking
 //   --host-validation  payload written/checked on the host + copies, as the reference
@@ -47,10 +52,12 @@
 
 #include "runner.hpp"
 #include "xorec_hip_bm.hpp"
+#include "xorec_hip_multi_bm.hpp"
 
 namespace {
 
 const char* kName = "XOR-EC (HIP gfx950)";
+const char* kNameMulti = "XOR-EC (HIP gfx950, multi-device)";
 
 size_t parse_size(const char* s) {
   char* end = nullptr;
@@ -79,17 +86,19 @@ std::vector<std::string> arg_vector(const char* s) {
 
 void usage() {
   std::printf(
-      "usage: xec_bench -g xorec-hip [-f out.csv] [-a] [-i iters] [-w warmup] [-s simd,...]\n"
+      "usage: xec_bench -g xorec-hip[,xorec-hip-multi] [-f out.csv] [-a] [-i iters] [-w warmup]\n"
+      "                 [-s simd,...]\n"
       "  -f, --file FILE        output CSV (must contain .csv; default results.csv)\n"
       "  -a, --append           append rows, no header (default: overwrite + header)\n"
       "  -i, --iterations N     timed iterations per config (default 10)\n"
       "  -w, --warmup N         warm-up iterations per config (default 0)\n"
-      "  -g, --gpu LIST         GPU algorithms: xorec-hip\n"
+      "  -g, --gpu LIST         GPU algorithms: xorec-hip, xorec-hip-multi\n"
       "  -c, --cpu LIST         CPU algorithms: none in this build\n"
       "  -s, --simd LIST        scalar,sse2,avx2,avx512 (CPU variants only; no effect)\n"
       "  -h, --help\n"
       "extensions: --message B --block B --data K --parity M --lost L | --sweep FILE\n"
-      "            --threads N --device D --seed S --sync MODE --host-validation --stdout\n"
+      "            --threads N --device D --devices LIST --seed S --sync MODE\n"
+      "            --host-validation --stdout\n"
       "without config options -g runs the reference's GPU sweep (get_gpu_configs)\n");
 }
 
@@ -128,7 +137,7 @@ std::vector<xec::BenchmarkConfig> gpu_sweep(const xec::BenchmarkConfig& base) {
 
 int main(int argc, char** argv) {
   enum { kMessage = 1000, kBlock, kData, kParity, kLost, kSweep, kThreads, kDevice, kSeed, kSync,
-         kHostVal, kStdout };
+         kHostVal, kStdout, kDevices };
   const option long_options[] = {
       {"help", no_argument, nullptr, 'h'},
       {"file", required_argument, nullptr, 'f'},
@@ -150,6 +159,7 @@ int main(int argc, char** argv) {
       {"sync", required_argument, nullptr, kSync},
       {"host-validation", no_argument, nullptr, kHostVal},
       {"stdout", no_argument, nullptr, kStdout},
+      {"devices", required_argument, nullptr, kDevices},
       {nullptr, 0, nullptr, 0}};
 
   xec::BenchmarkConfig base;
@@ -166,7 +176,8 @@ int main(int argc, char** argv) {
   single.block_size = 1u << 20;
   single.message_size = 256ull * 16 * (1u << 20);
   single.num_lost_blocks = 1;
-  bool single_mode = false, overwrite = true, to_stdout = false, gpu_selected = false;
+  bool single_mode = false, overwrite = true, to_stdout = false;
+  std::vector<std::string> algorithms;  // selected GPU algorithms, in -g order
   std::string out_file = "results.csv", sweep;
 
   int c, idx = 0;
@@ -192,8 +203,9 @@ int main(int argc, char** argv) {
         break;
       case 'g':
         for (const auto& a : arg_vector(optarg)) {
-          if (a != "xorec-hip") fail("Invalid GPU algorithm: " + a);
-          gpu_selected = true;
+          if (a != "xorec-hip" && a != "xorec-hip-multi") fail("Invalid GPU algorithm: " + a);
+          if (std::find(algorithms.begin(), algorithms.end(), a) == algorithms.end())
+            algorithms.push_back(a);
         }
         break;
       case 's':
@@ -213,10 +225,20 @@ int main(int argc, char** argv) {
       case kSync: base.sync_mode = std::atoi(optarg); break;
       case kHostVal: base.host_validation = true; break;
       case kStdout: to_stdout = true; break;
+      case kDevices:
+        base.devices.clear();
+        for (const auto& d : arg_vector(optarg)) {
+          char* end = nullptr;
+          const long v = std::strtol(d.c_str(), &end, 10);
+          if (d.empty() || *end != '\0' || v < 0) fail("Invalid device: " + d);
+          base.devices.push_back(static_cast<int>(v));
+        }
+        break;
       default: usage(); return EXIT_FAILURE;
     }
   }
-  if (!gpu_selected) fail("No benchmarks selected. Use --gpu xorec-hip to select the benchmark.");
+  if (algorithms.empty())
+    fail("No benchmarks selected. Use --gpu xorec-hip (or xorec-hip-multi) to select one.");
 
   std::vector<xec::BenchmarkConfig> cfgs;
   auto with_base = [&](xec::BenchmarkConfig x) {
@@ -226,6 +248,7 @@ int main(int argc, char** argv) {
     x.seed = base.seed;
     x.sync_mode = base.sync_mode;
     x.host_validation = base.host_validation;
+    x.devices = base.devices;
     return x;
   };
   if (!sweep.empty()) {
@@ -269,15 +292,20 @@ int main(int argc, char** argv) {
     if (overwrite) xec::write_csv_header(*os);
     int rc = 0;
     size_t n = 0;
-    for (const auto& x : cfgs) {
-      xec::RunResult r = xec::run_generic<xec::XorecBenchmarkHip>(kName, x);
-      xec::write_csv_row(*os, r, x);
-      os->flush();
-      std::fprintf(stderr, "[%zu/%zu] bs=%zu EC=(%zu/%zu) lost=%zu enc %.1f Gbit/s dec %.1f Gbit/s %s\n",
-                   ++n, cfgs.size(), x.block_size, std::get<0>(x.ec_params),
-                   std::get<1>(x.ec_params), x.num_lost_blocks, r.encode.tp_mean,
-                   r.decode.tp_mean, r.err_msg.c_str());
-      if (!r.err_msg.empty()) rc = 1;
+    for (const auto& alg : algorithms) {
+      const bool multi = alg == "xorec-hip-multi";
+      for (const auto& x : cfgs) {
+        xec::RunResult r = multi ? xec::run_generic<xec::XorecBenchmarkHipMulti>(kNameMulti, x)
+                                 : xec::run_generic<xec::XorecBenchmarkHip>(kName, x);
+        xec::write_csv_row(*os, r, x);
+        os->flush();
+        std::fprintf(stderr,
+                     "[%zu/%zu] %s bs=%zu EC=(%zu/%zu) lost=%zu enc %.1f Gbit/s dec %.1f Gbit/s %s\n",
+                     ++n, cfgs.size() * algorithms.size(), alg.c_str(), x.block_size,
+                     std::get<0>(x.ec_params), std::get<1>(x.ec_params), x.num_lost_blocks,
+                     r.encode.tp_mean, r.decode.tp_mean, r.err_msg.c_str());
+        if (!r.err_msg.empty()) rc = 1;
+      }
     }
     return rc;
   } catch (const std::exception& e) {

@@ -250,7 +250,9 @@ int xec_decode_tiling_used(void);
  * them chunk by chunk: H2D -> kernel -> D2H, chunks overlapping across
  * streams.  Host buffers should be pinned (hipHostMalloc / registered) for the
  * copies to be asynchronous; the calls return when the results are in host
- * memory.  Same argument checks and status codes as xec_encode / xec_decode. */
+ * memory.  Each call runs on the pipeline's device and leaves the caller's
+ * current device as it found it.  Same argument checks and status codes as
+ * xec_encode / xec_decode. */
 typedef struct xec_pipeline xec_pipeline;
 
 xec_status xec_pipeline_create(xec_pipeline** out, size_t chunk_stripes, size_t bs, size_t k,

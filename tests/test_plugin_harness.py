@@ -59,6 +59,10 @@ def test_cli_contract_errors():
     assert r.returncode == 1 and "warmup" in r.stderr
     r = run("-g", "xorec-hip", "--data", "4", "--parity", "1", "--lost", "2")
     assert r.returncode == 2 and "parity" in r.stderr
+    r = run("-g", "xorec-hip-multi", "--devices", "0,x")
+    assert r.returncode == 1 and "Invalid device" in r.stderr
+    r = run("-g", "xorec-hip-multi", "--devices", "0,-1")
+    assert r.returncode == 1 and "Invalid device" in r.stderr
 
 
 @pytest.mark.gpu
@@ -129,3 +133,34 @@ def test_harness_rows_clean(args):
     lost = int(row["lost_blocks"])
     if lost:
         assert float(row["decode_throughput_Gbps"]) > 0
+
+
+MULTI_EQUIV = ROOT / "tests" / "host" / "bin" / "multi_equiv"
+
+
+@pytest.mark.gpu
+def test_multi_device_plugin_matches_single_device():
+    """XorecBenchmarkHipMulti over device lists that repeat device 0 (2-4
+    stripe ranges with their own streams and buffers, uneven and empty ranges)
+    gives the one-device plugin's bytes after encode, erasure and decode
+    (tests/host/multi_equiv.cpp, built by __graft_entry__.build())."""
+    assert MULTI_EQUIV.exists(), "build with make -C tests/host"
+    p = subprocess.run([str(MULTI_EQUIV)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "multi_equiv ok" in p.stdout, p.stdout + p.stderr
+
+
+@pytest.mark.gpu
+def test_multi_device_rows_clean():
+    """`-g xorec-hip,xorec-hip-multi --devices 0,0,0`: one clean row per
+    algorithm, in -g order (get_benchmarks, benchmark_suite.cpp:279-311); the
+    multi-device run validates every block after erase + decode."""
+    r = run("-g", "xorec-hip,xorec-hip-multi", "--devices", "0,0,0", "--stdout", "--message", "64M",
+            "--block", "64K", "--data", "8", "--parity", "4", "--lost", "4", "-i", "3", "-w", "1",
+            "--seed", "3")
+    assert r.returncode == 0, r.stderr + r.stdout
+    rows = [dict(zip(HEADER, x)) for x in list(csv.reader(io.StringIO(r.stdout)))[1:]]
+    assert [x["name"] for x in rows] == ["XOR-EC (HIP gfx950)",
+                                         "XOR-EC (HIP gfx950, multi-device)"]
+    for x in rows:
+        assert x["err_msg"] == "", x
+        assert float(x["encode_throughput_Gbps"]) > 0 and float(x["decode_throughput_Gbps"]) > 0
