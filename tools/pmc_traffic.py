@@ -65,6 +65,12 @@ def main():
         base = name.split("<")[0]
         if base not in algo:
             continue
+        # only the headline launches (default shape, one granule per lane): the
+        # bench's host-pipeline / scatter legs run two granules per lane
+        # (<NM, 2, ...>) on other batch sizes, so their bytes are not these
+        targs = [a.strip() for a in name.split("<", 1)[1].rstrip(">").split(",")]
+        if len(targs) > 1 and targs[1] != "1":
+            continue
         f_kib = sum(fetch[name]) / len(fetch[name])
         w_kib = sum(write[name]) / len(write[name])
         hbm = int(round((2 * f_kib + w_kib) * 1024))
