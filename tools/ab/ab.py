@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--lost", type=int, default=1, help="lost data blocks per stripe (1..m)")
     ap.add_argument("--tiling", type=int, default=0,
                     help="xec_set_decode_tiling for every lib (0 = automatic)")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the identical-results check (diagnostic builds that store elsewhere)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -97,7 +99,7 @@ def main():
         got = (p.clone(), d.clone())
         if ref is None:
             ref = got
-        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), n
+        assert args.no_check or (torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])), n
     del ref, got
 
     def run(fn):
