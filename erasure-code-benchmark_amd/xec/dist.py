@@ -27,6 +27,16 @@ def _dist():
     return dist
 
 
+def _batch(ops):
+    """Post `ops` as one batch and wait.  Both ends of every transfer go
+    through batch_isend_irecv: with RCCL a batched op runs on the group's own
+    communicator, while a plain send / recv would run on a separate two-rank
+    communicator that the peer's batched op never joins."""
+    dist = _dist()
+    for w in (dist.batch_isend_irecv(ops) if ops else []):
+        w.wait()
+
+
 def scatter_stripes(full, local, S_total: int, stripe_bytes: int, root: int = 0):
     """Copy stripes [start, stop) of ``full`` (uint8, S_total*stripe_bytes, only
     read on ``root``) into ``local`` (uint8, (stop-start)*stripe_bytes) on every
@@ -42,12 +52,11 @@ def scatter_stripes(full, local, S_total: int, stripe_bytes: int, root: int = 0)
                 local.copy_(piece)
             elif b > a:
                 ops.append(dist.P2POp(dist.isend, piece, r))
-        for w in (dist.batch_isend_irecv(ops) if ops else []):
-            w.wait()
+        _batch(ops)
     else:
         a, b = stripe_range(S_total, rank, world)
         if b > a:
-            dist.recv(local, src=root)
+            _batch([dist.P2POp(dist.irecv, local, root)])
     return local
 
 
@@ -65,12 +74,11 @@ def gather_stripes(local, full, S_total: int, stripe_bytes: int, root: int = 0):
                 piece.copy_(local)
             elif b > a:
                 ops.append(dist.P2POp(dist.irecv, piece, r))
-        for w in (dist.batch_isend_irecv(ops) if ops else []):
-            w.wait()
+        _batch(ops)
     else:
         a, b = stripe_range(S_total, rank, world)
         if b > a:
-            dist.send(local, dst=root)
+            _batch([dist.P2POp(dist.isend, local, root)])
     return full
 
 
