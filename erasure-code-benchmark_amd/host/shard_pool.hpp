@@ -1,0 +1,80 @@
+// shard_pool.hpp -- one worker thread per device shard of XorecBenchmarkHipMulti.
+//
+// run(fn) calls fn(i) for every shard i at once -- shard 0 on the calling
+// thread, shard i > 0 on worker i -- and returns when all calls have.  Used
+// for decode(), whose xec_decode scans each shard's bitmap slice on the host
+// before it launches (~1.1 ns per stripe): on one thread device i would launch
+// only after the scans of devices 0..i-1 (config 4 over 8 devices: ~65 us of
+// skew against a ~180 us kernel).  The workers live as long as the plugin and
+// sleep on a condition variable between calls.
+#pragma once
+
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace xec {
+
+class ShardPool {
+ public:
+  explicit ShardPool(size_t shards) : n_(shards) {
+    for (size_t i = 1; i < n_; ++i) threads_.emplace_back([this, i] { worker(i); });
+  }
+  ~ShardPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    go_.notify_all();
+    for (std::thread& t : threads_) t.join();
+  }
+  ShardPool(const ShardPool&) = delete;
+  ShardPool& operator=(const ShardPool&) = delete;
+
+  // fn must not throw (the plugin's callbacks are noexcept C-ABI calls).
+  void run(const std::function<void(size_t)>& fn) {
+    if (n_ == 0) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &fn;
+      pending_ = n_ - 1;
+      ++gen_;
+    }
+    go_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void worker(size_t i) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      go_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      const std::function<void(size_t)>* job = job_;
+      lk.unlock();
+      (*job)(i);
+      lk.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+
+  size_t n_;
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable go_, done_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  size_t pending_ = 0;
+  bool stop_ = false;
+};
+
+}  // namespace xec

@@ -71,10 +71,12 @@ XorecBenchmarkHipMulti::XorecBenchmarkHipMulti(const BenchmarkConfig& config)
     s.d_erase = device_buffer(s.count * m_chunk_tot_blocks, "hipMalloc erase bitmap");
     s.d_bad = device_buffer(sizeof(uint32_t), "hipMalloc bad counter");
   }
+  m_pool = std::make_unique<ShardPool>(n);
 }
 
 XorecBenchmarkHipMulti::~XorecBenchmarkHipMulti() noexcept {
   const DeviceRestore restore;
+  m_pool.reset();  // join the workers before the streams they use go
   for (Shard& s : m_shards) {
     if (s.stream == nullptr) continue;
     (void)hipSetDevice(s.device);
@@ -124,21 +126,30 @@ int XorecBenchmarkHipMulti::encode() noexcept {
 }
 
 // Every shard decodes its slice of the host bitmap (xec_decode: host scan,
-// then the launch); the launches overlap across devices.  A shard with an
+// then the launch), each on its own thread (m_pool), so no device's launch
+// waits for another's scan; then every stream is waited for.  A shard with an
 // unrecoverable stripe fails alone -- the others are still rebuilt, as the
 // reference's GPU decode is all-or-nothing only per call (xorec_gpu_cmp.cu:75-81).
 int XorecBenchmarkHipMulti::decode() noexcept {
-  int status = XEC_SUCCESS;
-  const bool ok = each([&](const Shard& s) {
-    const xec_status st =
-        xec_decode(s.data.get(), s.parity.get(), s.count, m_block_size, m_chunk_data_blocks,
-                   m_chunk_parity_blocks, m_block_bitmap.get() + s.first * m_chunk_tot_blocks,
-                   s.d_bitmap.get(), s.stream);
-    if (st != XEC_SUCCESS && status == XEC_SUCCESS) status = st;
-    return st == XEC_SUCCESS;
+  const size_t n = m_shards.size();
+  std::vector<int> st(n, XEC_DEVICE_ERROR);
+  m_pool->run([&](size_t i) {
+    const Shard& s = m_shards[i];
+    const DeviceRestore restore;
+    if (hipSetDevice(s.device) != hipSuccess) return;
+    st[i] = xec_decode(s.data.get(), s.parity.get(), s.count, m_block_size, m_chunk_data_blocks,
+                       m_chunk_parity_blocks, m_block_bitmap.get() + s.first * m_chunk_tot_blocks,
+                       s.d_bitmap.get(), s.stream);
   });
+  const bool ok = each([](const Shard&) { return true; });  // wait for every stream
+  int status = XEC_SUCCESS;
+  for (int v : st)
+    if (v != XEC_SUCCESS) {
+      status = v;
+      break;
+    }
   m_last_status = status;
-  return ok ? 0 : -1;
+  return ok && status == XEC_SUCCESS ? 0 : -1;
 }
 
 // AbstractBenchmark::simulate_data_loss (abstract_bm.cpp:20-39): erasure sets

@@ -20,9 +20,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <vector>
 
 #include "abstract_bm.hpp"
+#include "shard_pool.hpp"
 
 namespace xec {
 
@@ -69,6 +71,7 @@ class XorecBenchmarkHipMulti : public AbstractBenchmark {
   // m_block_bitmap: pinned host S*(k+m) for the whole batch (base-class
   // member, replaced in the constructor); m_data_buf / m_parity_buf unused.
   std::vector<Shard> m_shards;
+  std::unique_ptr<ShardPool> m_pool;  // decode(): one thread per shard (shard_pool.hpp)
   int m_last_status = 0;
 };
 

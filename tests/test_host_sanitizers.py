@@ -39,3 +39,18 @@ def test_oracle_asan_ubsan(tmp_path):
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert "oracle_asan ok" in p.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_shard_pool_tsan(tmp_path):
+    """The multi-device plugin's per-shard decode threads (host/shard_pool.hpp)
+    under ThreadSanitizer: each run calls every shard once and returns after
+    all of them, over 2,000 runs per pool size."""
+    exe = tmp_path / "shard_pool_test"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+                    f"-I{ROOT / 'erasure-code-benchmark_amd' / 'host'}",
+                    str(ROOT / "tests" / "host" / "shard_pool_test.cpp"), "-o", str(exe)],
+                   check=True, capture_output=True)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert "shard_pool ok" in p.stdout
