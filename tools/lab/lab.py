@@ -34,6 +34,9 @@ def main():
                     help="--decode: diagnostics store their result sc1 (the product's policy)")
     ap.add_argument("--wburst", action="store_true",
                     help="time write-only bursts of 1/4/16 KiB per workgroup, nt vs sc1")
+    ap.add_argument("--wscatter", action="store_true",
+                    help="time scattered write-only streams (the decode's rebuilt-block "
+                         "pattern) against a dense one, nt and sc1")
     ap.add_argument("--occ", default="0", help="--ceiling: waves-per-SIMD caps (0 = none), "
                                                "crossed with the product encode's own setting")
     args = ap.parse_args()
@@ -75,6 +78,8 @@ def main():
         return ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh)
     if args.wburst:
         return wburst_lab(args, L, torch, sets, S, k, bs, s, sh)
+    if args.wscatter:
+        return wscatter_lab(args, L, torch, sets, S, k, bs, s, sh)
 
     # correctness of every variant first
     bad = []
@@ -247,6 +252,50 @@ def wburst_lab(args, L, torch, sets, S, k, bs, s, sh):
         print(f"{n:16s} {out[n]}", flush=True)
     if args.out:
         Path(args.out).write_text(json.dumps({"bytes": nbytes, "results": out}, indent=1))
+
+
+def wscatter_lab(args, L, torch, sets, S, k, bs, s, sh):
+    """Write-only streams of up to 1 GiB into the data buffers: dense, and as the
+    decode's rebuilt blocks land -- one block per stripe (config 3: 1 MiB per
+    16 MiB; 16+8 x 64 KiB: 64 KiB per 1.5 MiB; config 4: 4 KiB per 132 KiB),
+    each as one-wave 1 KiB stores; nt and sc1.  Overwrites the data buffers."""
+    L.lab_wscatter.argtypes = [ctypes.c_int, ctypes.c_void_p] + [ctypes.c_uint64] * 3 + [ctypes.c_void_p]
+    total = 1 << 30
+    span = S * k * bs
+    shapes = {"dense_1M": (1 << 20, 1 << 20), "cfg3_1M_per_16M": (1 << 20, 16 << 20),
+              "m8_64K_per_1.5M": (64 << 10, 1536 << 10), "cfg4_4K_per_132K": (4 << 10, 132 << 10),
+              "4K_per_16K": (4 << 10, 16 << 10), "64K_per_128K": (64 << 10, 128 << 10)}
+    cases = []
+    for name, (blk, stride) in shapes.items():
+        nblk = total // blk
+        if (nblk - 1) * stride + blk > span:
+            nblk = (span - blk) // stride + 1
+        for sc1 in (0, 1):
+            cases.append((f"{name}_{'sc1' if sc1 else 'nt'}", sc1, blk, stride, nblk))
+
+    def run(fn):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.iters)]
+        fn(0)
+        for i in range(args.iters):
+            ev[2 * i].record(s)
+            fn(i + 1)
+            ev[2 * i + 1].record(s)
+        torch.cuda.synchronize()
+        return [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.iters)]
+
+    res = {c[0]: [] for c in cases}
+    for _ in range(args.rounds):
+        for name, sc1, blk, stride, nblk in cases:
+            res[name] += run(lambda i, a=(sc1, blk, stride, nblk): L.lab_wscatter(
+                a[0], sets[i % 2][0].data_ptr(), a[1], a[2], a[3], sh))
+    out = {}
+    for name, sc1, blk, stride, nblk in cases:
+        med = statistics.median(res[name])
+        out[name] = {"block": blk, "stride": stride, "blocks": nblk, "bytes": nblk * blk,
+                     "ms_med": round(med, 4), "GBps_med": round(nblk * blk / (med * 1e-3) / 1e9, 1)}
+        print(f"{name:24s} {out[name]}", flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps(out, indent=1))
 
 
 def ceiling_lab(args, L, torch, xec, sets, S, k, m, bs, s, sh):

@@ -321,6 +321,19 @@ __global__ __launch_bounds__(T) void wburst_wg(uint8_t* out, uint64_t total_byte
   __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)(threadIdx.x * 16), 0, 2);
 }
 
+// write-only, scattered: nblk blocks of blk bytes, block b at byte b*stride;
+// one-wave workgroup per 1 KiB (the decode's rebuilt-block store shape).
+template <int AUX>
+__global__ __launch_bounds__(64) void wscatter(uint8_t* out, uint64_t blk, uint64_t stride,
+                                               uint64_t nblk) {
+  const uint64_t per = blk / 1024, t = blockIdx.x;
+  if (t >= nblk * per) return;
+  uint8_t* base = out + (t / per) * stride + (t % per) * 1024;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  u32x4 v = {(uint32_t)t, threadIdx.x, 0x9E3779B9u, 0x7F4A7C15u};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)(threadIdx.x * 16), 0, AUX);
+}
+
 // one-wave workgroups that process TPW ADJACENT tiles in sequence (tile
 // b*TPW + i): the store of tile i overlaps the loads of tile i+1.
 template <int NM, int TPW>
@@ -575,6 +588,18 @@ int lab_wburst(int v, void* out, uint64_t bytes, hipStream_t s) {
     case 11: wburst_xcd<2, 2><<<grid(1), 64, lds, s>>>(o, bytes); break;
     default: return 1;
   }
+  return hipGetLastError() == hipSuccess ? 0 : 6;
+}
+
+// Scattered write-only stream (wscatter): sc1 = 1 -> sc1 stores, else nt.
+int lab_wscatter(int sc1, void* out, uint64_t blk, uint64_t stride, uint64_t nblk,
+                 hipStream_t s) {
+  if (blk < 1024 || blk % 1024 != 0 || stride < blk) return 1;
+  const uint64_t n = nblk * (blk / 1024);
+  if (n == 0 || n > 0x7fffffffu) return 1;
+  uint8_t* o = static_cast<uint8_t*>(out);
+  if (sc1) wscatter<16><<<(uint32_t)n, 64, g_ceiling_lds, s>>>(o, blk, stride, nblk);
+  else wscatter<2><<<(uint32_t)n, 64, g_ceiling_lds, s>>>(o, blk, stride, nblk);
   return hipGetLastError() == hipSuccess ? 0 : 6;
 }
 
