@@ -70,23 +70,29 @@ xec_status fail(xec_pipeline* p, xec_status st) {
   return st;
 }
 
-// Copy runs of consecutive blocks of stripe row `bm` (k data bytes) whose
-// bitmap byte is (lost ? 0 : nonzero) -- adjacent blocks merge into one copy.
-template <typename F>
-bool for_runs(const uint8_t* bm, size_t k, bool lost, F&& copy) {
+// Copy runs of consecutive indices i < n with want(i) -- adjacent blocks merge
+// into one copy.
+template <typename W, typename F>
+bool for_runs(size_t n, W&& want, F&& copy) {
   size_t i = 0;
-  while (i < k) {
-    if ((bm[i] == 0) != lost) {
+  while (i < n) {
+    if (!want(i)) {
       ++i;
       continue;
     }
     size_t j = i;
-    while (j < k && (bm[j] == 0) == lost) ++j;
+    while (j < n && want(j)) ++j;
     if (!copy(i, j)) return false;
     i = j;
   }
   return true;
 }
+
+// Blocks from this size on travel only where a rebuild reads them (the
+// members and parity of classes that lost a data block); smaller blocks
+// travel as whole runs of survivors, where one copy per block would cost more
+// in per-copy overhead than the bytes it saves.  With m = 1 both are the same.
+constexpr size_t kSelectiveCopyBytes = 64u << 10;
 
 }  // namespace
 
@@ -167,6 +173,8 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
   if (st != XEC_SUCCESS || !needs) return st;  // all-or-nothing, as xec_decode
   auto* data = static_cast<uint8_t*>(h_data);
   const auto* par = static_cast<const uint8_t*>(h_parity);
+  const bool selective = m > 1 && bs >= kSelectiveCopyBytes;
+  std::vector<uint8_t> class_lost(m);
   size_t chunk = 0;
   for (size_t c0 = 0; c0 < S; c0 += p->chunk_stripes, ++chunk) {
     auto& s = p->slots[chunk % p->slots.size()];
@@ -179,24 +187,37 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
           break;
         }
     if (!any_lost) continue;  // nothing of this chunk crosses the link
-    // H2D: only the surviving data blocks (a lost block's content is never
-    // read) and the chunk's parity; D2H: only the rebuilt blocks.
+    // H2D: the surviving data blocks a rebuild reads (a lost block's content
+    // is never read) and the parity; D2H: only the rebuilt blocks.  With
+    // selective copies only the classes that lost a data block travel
+    // (xorec.cpp:79-108 reads nothing else).
     for (size_t c = c0; c < c0 + n; ++c) {
+      const uint8_t* bm = h_bitmap + c * row;
       const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
-      if (!for_runs(h_bitmap + c * row, k, false, [&](size_t i, size_t j) {
-            return hipMemcpyAsync(s.data + sbase + i * bs, data + base + i * bs, (j - i) * bs,
-                                  hipMemcpyHostToDevice, s.stream) == hipSuccess;
-          }))
+      for (size_t j = 0; j < m; ++j) class_lost[j] = 0;
+      for (size_t i = 0; i < k; ++i)
+        if (bm[i] == 0) class_lost[i % m] = 1;
+      const auto h2d = [&](uint8_t* d, const uint8_t* h) {
+        return [&, d, h](size_t i, size_t j) {
+          return hipMemcpyAsync(d + i * bs, h + i * bs, (j - i) * bs, hipMemcpyHostToDevice,
+                                s.stream) == hipSuccess;
+        };
+      };
+      if (!for_runs(k, [&](size_t i) { return bm[i] != 0 && (!selective || class_lost[i % m]); },
+                    h2d(s.data + sbase, data + base)) ||
+          (selective && !for_runs(m, [&](size_t j) { return class_lost[j] != 0; },
+                                  h2d(s.parity + (c - c0) * m * bs, par + c * m * bs))))
         return fail(p, XEC_DEVICE_ERROR);
     }
-    if (hipMemcpyAsync(s.parity, par + c0 * m * bs, n * m * bs, hipMemcpyHostToDevice, s.stream) !=
-        hipSuccess)
+    if (!selective && hipMemcpyAsync(s.parity, par + c0 * m * bs, n * m * bs,
+                                     hipMemcpyHostToDevice, s.stream) != hipSuccess)
       return fail(p, XEC_DEVICE_ERROR);
     st = xec_decode(s.data, s.parity, n, bs, k, m, h_bitmap + c0 * row, s.bitmap, s.stream);
     if (st != XEC_SUCCESS) return fail(p, st);
     for (size_t c = c0; c < c0 + n; ++c) {
+      const uint8_t* bm = h_bitmap + c * row;
       const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
-      if (!for_runs(h_bitmap + c * row, k, true, [&](size_t i, size_t j) {
+      if (!for_runs(k, [&](size_t i) { return bm[i] == 0; }, [&](size_t i, size_t j) {
             return hipMemcpyAsync(data + base + i * bs, s.data + sbase + i * bs, (j - i) * bs,
                                   hipMemcpyDeviceToHost, s.stream) == hipSuccess;
           }))

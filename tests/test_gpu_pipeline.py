@@ -14,11 +14,14 @@ def _pinned(nbytes):
     return torch.empty(max(nbytes, 1), dtype=torch.uint8).pin_memory()
 
 
-@pytest.mark.parametrize("S,k,m,bs,chunk,ns", [
-    (37, 8, 1, 65536, 8, 2), (256, 16, 1, 1 << 20, 16, 3), (100, 12, 4, 4096, 7, 4),
-    (5, 4, 1, 4096, 16, 2), (64, 32, 8, 1024, 1, 1),
+@pytest.mark.parametrize("S,k,m,bs,chunk,ns,lost", [
+    (37, 8, 1, 65536, 8, 2, 1), (256, 16, 1, 1 << 20, 16, 3, 1), (100, 12, 4, 4096, 7, 4, 4),
+    (5, 4, 1, 4096, 16, 2, 1), (64, 32, 8, 1024, 1, 1, 8),
+    # m > 1 at >= 64 KiB blocks: only the classes that lost a data block travel
+    (40, 16, 4, 65536, 8, 3, 1), (24, 16, 4, 65536, 5, 2, 2), (12, 8, 2, 1 << 20, 4, 2, 2),
+    (9, 24, 8, 65536, 4, 3, 3),
 ])
-def test_pipeline_encode_decode(gpu, oracle, S, k, m, bs, chunk, ns):
+def test_pipeline_encode_decode(gpu, oracle, S, k, m, bs, chunk, ns, lost):
     ref_d, ref_p = oracle.batch(S, k, m, bs)
     h_d = _pinned(S * k * bs)
     h_p = _pinned(S * m * bs)
@@ -29,7 +32,7 @@ def test_pipeline_encode_decode(gpu, oracle, S, k, m, bs, chunk, ns):
         # erase a recoverable set in every other stripe; odd stripes keep all data
         bm = np.ones((S, k + m), np.uint8)
         for c in range(0, S, 2):
-            oracle.select_lost_blocks(k, m, m, bm[c], c)
+            oracle.select_lost_blocks(k, m, lost, bm[c], c)
         d = h_d.numpy().reshape(S, k, bs)
         d[bm[:, :k] == 0] = 0
         h_bm = _pinned(S * (k + m))

@@ -8,7 +8,7 @@ The batch starts and ends in pinned host memory.  Measured:
 Rates are in the reference's convention (data bytes / s, GB = 1e9), the
 natural unit for a path whose bytes cross PCIe once.
 
-    python tools/host_pipeline.py [--workload cfg3] [--reps 3] [--out f.json]
+    python tools/host_pipeline.py [--workload cfg3|k,m,bs,S] [--lost N] [--reps 3] [--out f.json]
 """
 from __future__ import annotations
 
@@ -23,7 +23,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 sys.path.insert(0, str(ROOT))
 
-from bench import WORKLOADS  # noqa: E402
+from bench import erasure_pattern, workload_shape  # noqa: E402
 
 
 def main():
@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunks", default="4,8,16,32")
     ap.add_argument("--streams", default="2,3,4")
+    ap.add_argument("--lost", type=int, default=1,
+                    help="lost data blocks per stripe, one per class (bench.py erasure_pattern)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -42,7 +44,7 @@ def main():
 
     torch.cuda.set_device(0)
     assert xec.init(0) == 0
-    k, m, bs, S, _ = WORKLOADS[args.workload]
+    k, m, bs, S, _ = workload_shape(args.workload)
     data_bytes = S * k * bs
     h_d = torch.empty(data_bytes, dtype=torch.uint8).pin_memory()
     h_p = torch.empty(S * m * bs, dtype=torch.uint8).pin_memory()
@@ -53,8 +55,7 @@ def main():
     h_d.copy_(d_d)
     assert xec.encode(d_d, d_p, S, bs, k, m, s) == 0
     ref_p = d_p.cpu()
-    bm = np.ones((S, k + m), np.uint8)
-    bm[np.arange(S), (7 * np.arange(S)) % k] = 0
+    bm = erasure_pattern(np, S, k, m, args.lost)
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     torch.cuda.synchronize()
 
@@ -68,7 +69,8 @@ def main():
             ts.append(time.perf_counter() - t0)
         return statistics.median(ts)
 
-    res = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S, "data_bytes": data_bytes}
+    res = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S, "lost": args.lost,
+           "data_bytes": data_bytes, "lib": str(xec.LIB_PATH)}
     t = timed(lambda: d_d.copy_(h_d, non_blocking=True))
     res["link_h2d_GBps"] = round(data_bytes / t / 1e9, 2)
     t = timed(lambda: h_d.copy_(d_d, non_blocking=True))
