@@ -58,7 +58,10 @@ def main():
     assert xec.init(0) == 0
     loaded = {n: load(n) for n in args.libs.split(",")}
     for L in loaded.values():
-        assert L.xec_set_decode_tiling(args.tiling) == 0
+        if hasattr(L, "xec_set_decode_tiling"):  # round-1 builds predate the call
+            assert L.xec_set_decode_tiling(args.tiling) == 0
+        else:
+            assert args.tiling == 0, "--tiling needs xec_set_decode_tiling"
     occs = [int(x) for x in args.occ.split(",")] if args.occ else [None]
     libs = {}
     for n, L in loaded.items():
