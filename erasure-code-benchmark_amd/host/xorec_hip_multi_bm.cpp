@@ -184,6 +184,45 @@ bool XorecBenchmarkHipMulti::check_for_corruption() const noexcept {
   return ok && std::all_of(bad.begin(), bad.end(), [](uint32_t b) { return b == 0; });
 }
 
+// Every shard device reads (scatter) or writes (gather) root's HBM: give it
+// peer access to root where the pair supports it (otherwise the runtime
+// stages the copy).  An access already enabled is fine.
+bool XorecBenchmarkHipMulti::enable_peer(int root) noexcept {
+  const DeviceRestore restore;
+  for (const Shard& s : m_shards) {
+    if (s.device == root) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, s.device, root) != hipSuccess) return false;
+    if (!can) continue;
+    if (hipSetDevice(s.device) != hipSuccess) return false;
+    const hipError_t e = hipDeviceEnablePeerAccess(root, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return false;
+    (void)hipGetLastError();  // clear a sticky "already enabled"
+  }
+  return true;
+}
+
+int XorecBenchmarkHipMulti::scatter_from(const uint8_t* d_root_data, int root) noexcept {
+  if (d_root_data == nullptr || !enable_peer(root)) return -1;
+  const bool ok = each([&](const Shard& s) {
+    return s.count == 0 ||
+           hipMemcpyPeerAsync(s.data.get(), s.device, d_root_data + s.first * m_chunk_data_size,
+                              root, s.count * m_chunk_data_size, s.stream) == hipSuccess;
+  });
+  return ok ? 0 : -1;
+}
+
+int XorecBenchmarkHipMulti::gather_parity_to(uint8_t* d_root_parity, int root) noexcept {
+  if (d_root_parity == nullptr || !enable_peer(root)) return -1;
+  const bool ok = each([&](const Shard& s) {
+    return s.count == 0 ||
+           hipMemcpyPeerAsync(d_root_parity + s.first * m_chunk_parity_size, root,
+                              s.parity.get(), s.device, s.count * m_chunk_parity_size,
+                              s.stream) == hipSuccess;
+  });
+  return ok ? 0 : -1;
+}
+
 bool XorecBenchmarkHipMulti::read_shard(size_t i, uint8_t* h_data, uint8_t* h_parity) const
     noexcept {
   if (i >= m_shards.size()) return false;

@@ -49,6 +49,17 @@ class XorecBenchmarkHipMulti : public AbstractBenchmark {
   // Copies shard i's data / parity slice to host memory (tests).
   bool read_shard(size_t i, uint8_t* h_data, uint8_t* h_parity) const noexcept;
 
+  // Config 5's exchange in one process: the batch starts
+  // in the HBM of `root` (S*k*bs bytes, the reference layout) and every
+  // shard's stripe range is copied to its device with hipMemcpyPeerAsync --
+  // xGMI DMA between GPUs, a device copy when shard and root share one --
+  // all shards at once on their own streams; returns when every copy has
+  // landed (0, or -1 on a HIP error).  Peer access to root is enabled where
+  // the devices allow it.  gather_parity_to is the inverse for the parity
+  // (S*m*bs bytes on root).  No collective: stripes are independent.
+  int scatter_from(const uint8_t* d_root_data, int root) noexcept;
+  int gather_parity_to(uint8_t* d_root_parity, int root) noexcept;
+
  protected:
   void m_write_data_buffer() noexcept override;
 
@@ -72,6 +83,7 @@ class XorecBenchmarkHipMulti : public AbstractBenchmark {
   // member, replaced in the constructor); m_data_buf / m_parity_buf unused.
   std::vector<Shard> m_shards;
   std::unique_ptr<ShardPool> m_pool;  // decode(): one thread per shard (shard_pool.hpp)
+  bool enable_peer(int root) noexcept;
   int m_last_status = 0;
 };
 

@@ -149,6 +149,20 @@ def test_multi_device_plugin_matches_single_device():
     assert p.returncode == 0 and "multi_equiv ok" in p.stdout, p.stdout + p.stderr
 
 
+MULTI_SCATTER = ROOT / "tests" / "host" / "bin" / "multi_scatter"
+
+
+@pytest.mark.gpu
+def test_multi_device_scatter_gather():
+    """Config 5's exchange in one process: a batch in device 0's HBM scattered
+    over the shards with peer copies, encoded per shard, parity gathered back
+    == device 0's own encode; shard data == its range of the root batch
+    (tests/host/multi_scatter.cpp; ragged, empty and single ranges)."""
+    assert MULTI_SCATTER.exists(), "build with make -C tests/host"
+    p = subprocess.run([str(MULTI_SCATTER)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "multi_scatter ok" in p.stdout, p.stdout + p.stderr
+
+
 @pytest.mark.gpu
 def test_multi_device_rows_clean():
     """`-g xorec-hip,xorec-hip-multi --devices 0,0,0`: one clean row per
