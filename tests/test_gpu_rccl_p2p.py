@@ -1,0 +1,53 @@
+"""RCCL point-to-point on the GPU box (one GPU): the batched send / recv that
+xec/dist.py's scatter and gather post (batch_isend_irecv on both ends) run
+over RCCL here as a send to self inside one batch, bit-exact, plus the
+world-1 scatter / gather (the root's own slice).  The N > 1 transfers between
+GPUs are the driver's 8-GPU runs; tests/test_distributed_cpu.py covers their
+bookkeeping under gloo."""
+from __future__ import annotations
+
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+SCRIPT = r"""
+import os, socket, sys
+sys.path.insert(0, sys.argv[1])
+import torch
+import torch.distributed as dist
+from xec import dist as xdist
+with socket.socket() as s:
+    s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
+                        init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+g = torch.Generator(device="cuda").manual_seed(7)
+src = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device="cuda", generator=g)
+dst = torch.zeros_like(src)
+xdist._batch([dist.P2POp(dist.isend, src, 0), dist.P2POp(dist.irecv, dst, 0)])
+torch.cuda.synchronize()
+assert torch.equal(src, dst), "self send/recv"
+S, sb = 12, 4096
+full = torch.randint(0, 256, (S * sb,), dtype=torch.uint8, device="cuda", generator=g)
+local = torch.empty_like(full)
+xdist.scatter_stripes(full, local, S, sb)
+back = torch.zeros_like(full)
+xdist.gather_stripes(local, back, S, sb)
+torch.cuda.synchronize()
+assert torch.equal(full, local) and torch.equal(full, back), "world-1 scatter / gather"
+print("backend", dist.get_backend(), "ranks", dist.get_world_size())
+dist.destroy_process_group()
+print("rccl p2p ok")
+"""
+
+
+def test_rccl_batched_p2p_self():
+    p = subprocess.run([sys.executable, "-c", SCRIPT, str(ROOT / "erasure-code-benchmark_amd")],
+                       capture_output=True, text=True, timeout=300, cwd=str(ROOT))
+    assert p.returncode == 0 and "rccl p2p ok" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
+    assert "backend nccl" in p.stdout
