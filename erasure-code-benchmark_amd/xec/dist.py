@@ -19,12 +19,35 @@ metric (DESIGN.md).
 """
 from __future__ import annotations
 
+import os
+
 from .partition import stripe_range
+
+# Largest single point-to-point message.  RCCL 2.26 (torch 2.10's bundled
+# librccl) returned a send-to-self of more than 1 GiB with its second half
+# wrong and no error (tools/rccl/p2p_size_probe.py, profiles/r02bf), and
+# config 5 sends 4 GiB per peer; every transfer is therefore posted as pieces
+# of at most this many bytes, in offset order on both ends (matched pairwise
+# in order).  XEC_P2P_PIECE_BYTES overrides it (tests).
+P2P_PIECE_BYTES = 256 << 20
+
+
+def _piece_bytes() -> int:
+    return int(os.environ.get("XEC_P2P_PIECE_BYTES", P2P_PIECE_BYTES))
 
 
 def _dist():
     import torch.distributed as dist
     return dist
+
+
+def p2p_ops(op, tensor, peer):
+    """P2POps moving the 1-D ``tensor`` to / from ``peer`` in pieces of at most
+    :data:`P2P_PIECE_BYTES` bytes."""
+    dist = _dist()
+    step = max(1, _piece_bytes() // max(1, tensor.element_size()))
+    n = tensor.numel()
+    return [dist.P2POp(op, tensor[i:i + step], peer) for i in range(0, n, step)]
 
 
 def _batch(ops):
@@ -51,12 +74,12 @@ def scatter_stripes(full, local, S_total: int, stripe_bytes: int, root: int = 0)
             if r == root:
                 local.copy_(piece)
             elif b > a:
-                ops.append(dist.P2POp(dist.isend, piece, r))
+                ops += p2p_ops(dist.isend, piece, r)
         _batch(ops)
     else:
         a, b = stripe_range(S_total, rank, world)
         if b > a:
-            _batch([dist.P2POp(dist.irecv, local, root)])
+            _batch(p2p_ops(dist.irecv, local, root))
     return local
 
 
@@ -73,12 +96,12 @@ def gather_stripes(local, full, S_total: int, stripe_bytes: int, root: int = 0):
             if r == root:
                 piece.copy_(local)
             elif b > a:
-                ops.append(dist.P2POp(dist.irecv, piece, r))
+                ops += p2p_ops(dist.irecv, piece, r)
         _batch(ops)
     else:
         a, b = stripe_range(S_total, rank, world)
         if b > a:
-            _batch([dist.P2POp(dist.isend, local, root)])
+            _batch(p2p_ops(dist.isend, local, root))
     return full
 
 

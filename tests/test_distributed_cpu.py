@@ -59,9 +59,15 @@ def _worker(rank, world, port, S, k, m, bs, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,S", [(2, 9), (2, 2), (3, 10), (3, 2), (4, 9), (8, 20), (8, 5)])
-def test_partitioned_encode_matches_single_process(world, S):
+@pytest.mark.parametrize("world,S,piece", [(2, 9, 0), (2, 2, 0), (3, 10, 0), (3, 2, 0), (4, 9, 0),
+                                           (8, 20, 0), (8, 5, 0),
+                                           # transfers split into ragged pieces (xec/dist.py
+                                           # P2P_PIECE_BYTES): 1000 B against 4 KiB stripes
+                                           (3, 10, 1000), (4, 9, 4096)])
+def test_partitioned_encode_matches_single_process(world, S, piece, monkeypatch):
     k, m, bs = 8, 2, 512
+    if piece:  # inherited by the spawned ranks
+        monkeypatch.setenv("XEC_P2P_PIECE_BYTES", str(piece))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

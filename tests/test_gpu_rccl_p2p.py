@@ -27,11 +27,13 @@ torch.cuda.set_device(0)
 dist.init_process_group("nccl", device_id=torch.device("cuda", 0),
                         init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
 g = torch.Generator(device="cuda").manual_seed(7)
-src = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device="cuda", generator=g)
-dst = torch.zeros_like(src)
-xdist._batch([dist.P2POp(dist.isend, src, 0), dist.P2POp(dist.irecv, dst, 0)])
-torch.cuda.synchronize()
-assert torch.equal(src, dst), "self send/recv"
+for n in (64 << 20, (4 << 30) + 4096):  # config 5 sends 4 GiB per peer: past 2^32 bytes
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    dst = torch.zeros_like(src)
+    xdist._batch(xdist.p2p_ops(dist.isend, src, 0) + xdist.p2p_ops(dist.irecv, dst, 0))
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst), f"self send/recv of {n} bytes in pieces"
+    del src, dst
 S, sb = 12, 4096
 full = torch.randint(0, 256, (S * sb,), dtype=torch.uint8, device="cuda", generator=g)
 local = torch.empty_like(full)
