@@ -89,6 +89,7 @@ int main() {
       {37, 8, 4, 65536, {0, 0, 0}},        // ragged ranges, m > 1
       {2, 4, 2, 4096, {0, 0, 0, 0, 0}},    // empty ranges
       {16, 32, 1, 4096, {0}},              // one shard: the copy is the whole batch
+      {288, 16, 1, 1 << 20, {0}},          // one 4.5 GiB copy: offsets and sizes past 2^32
   };
   for (const Case& c : cases) {
     const int rc = check(c.S, c.k, c.m, c.bs, c.devices);
