@@ -35,7 +35,9 @@ class ShardPool {
   ShardPool(const ShardPool&) = delete;
   ShardPool& operator=(const ShardPool&) = delete;
 
-  // fn must not throw (the plugin's callbacks are noexcept C-ABI calls).
+  // fn must not throw (the plugin's callbacks are noexcept C-ABI calls).  One
+  // caller at a time: run() is not reentrant (the plugin calls it from
+  // decode() only).
   void run(const std::function<void(size_t)>& fn) {
     if (n_ == 0) return;
     {
