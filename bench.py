@@ -446,7 +446,19 @@ def main():
     run_rank(args)
 
 
+def _result_stream():
+    """The one JSON line goes to the process's stdout; everything else written
+    to fd 1 from here on -- RCCL prints a version banner there at communicator
+    init, once per rank -- is sent to stderr, so stdout carries exactly the
+    result line at any N."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def run_rank(args):
+    result_out = _result_stream()
     import torch
     import torch.distributed as dist
 
@@ -763,7 +775,7 @@ def run_rank(args):
                 for leg, on in (("host_pipeline", host_leg), ("scatter", scatter_leg)):
                     if on and leg not in out:
                         out[leg] = {"error": f"timed out ({args.scatter_timeout:.0f} s watchdog)"}
-                print(json.dumps(out), flush=True)
+                print(json.dumps(out), file=result_out, flush=True)
             sys.stderr.flush()
             os._exit(3)
 
@@ -815,7 +827,7 @@ def run_rank(args):
         if not args.rehearse_cpu:
             xec.set_launch(0, 0, 0, 0)
     if out is not None:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     if use_dist:
         dist.destroy_process_group()
     if bad:

@@ -21,8 +21,10 @@ def run_bench(*args):
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True,
                        text=True, timeout=600, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout
+    # stdout carries exactly the result line (RCCL's init banner and any other
+    # library output go to stderr: bench.py _result_stream)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
     return json.loads(lines[0])
 
 

@@ -28,8 +28,8 @@ def test_launcher_plain_command(n):
     p = _bench("--gpus", str(n), "--rehearse-cpu", "--dist-backend", "gloo",
                "--workload", "8,2,4096,5", "--steps", "3", "--warmup", "1")
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout  # rank 0 only
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout  # rank 0's line, nothing else
     out = json.loads(lines[0])
     assert out["n_gpus"] == n
     assert out["dist"] == {"backend": "gloo", "ranks_seen": n, "launcher": "bench.py"}
