@@ -3,12 +3,20 @@ plus the block-size extreme where the kernels leave the 32-bit buffer-offset
 store path (bs > 2 GiB, xec_api.cpp launch_shape)."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
 from test_gpu_parity import encode_and_check, erase_decode_check
 
 pytestmark = pytest.mark.gpu
+
+# Case counts and a seed offset for longer runs on the GPU box (defaults are the
+# suite's): XEC_FUZZ_CASES=400 XEC_FUZZ_SEED=10000 pytest tests/test_gpu_fuzz.py -m gpu
+N_SHAPE_CASES = int(os.environ.get("XEC_FUZZ_CASES", "48"))
+N_PATH_CASES = int(os.environ.get("XEC_FUZZ_CASES", "24"))
+SEED_OFFSET = int(os.environ.get("XEC_FUZZ_SEED", "0"))
 
 LAUNCH_SHAPES = [(0, 0, 0, 0), (1, 0, 1, 64), (2, 0, 1, 64), (1, 0, 2, 256), (2, 4096, 1, 256),
                  (1, 777, 2, 64)]
@@ -22,8 +30,9 @@ def _random_case(rng):
     return S, k, m, bs
 
 
-@pytest.mark.parametrize("case", range(48))
+@pytest.mark.parametrize("case", range(N_SHAPE_CASES))
 def test_random_shape_and_launch_shape(gpu, oracle, case):
+    case += SEED_OFFSET
     rng = np.random.default_rng(4242 + case)
     S, k, m, bs = _random_case(rng)
     shape = LAUNCH_SHAPES[case % len(LAUNCH_SHAPES)]
@@ -109,7 +118,7 @@ def _decode_via(gpu, path, b, h_bm, d_bm):
     return int(st.item())
 
 
-@pytest.mark.parametrize("case", range(24))
+@pytest.mark.parametrize("case", range(N_PATH_CASES))
 def test_random_shape_every_decode_path(gpu, oracle, case):
     """Every decode entry point and forced tiling on the same random shape and
     loss pattern, bit-exact against the oracle: the batch paths all-or-nothing
@@ -117,6 +126,7 @@ def test_random_shape_every_decode_path(gpu, oracle, case):
     (xorec_bm.cpp:43-58); parity never written.  k > 256 (the list's limit):
     the list-only entry points must refuse with InvalidSize and touch nothing."""
     import torch
+    case += SEED_OFFSET
     rng = np.random.default_rng(777 + case)
     S, k, m, bs = _random_case(rng)
     S = max(S, 3)
