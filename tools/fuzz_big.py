@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Randomised round trips at real batch sizes (GPU box): the size-independent
+property check of tests/test_gpu_fuzz.py, without the CPU oracle, so batches of
+128 MiB - 2 GiB fit.  Per case: a random k, m (k % m == 0), block size and
+stripe count; fill; encode, parity checked against a torch XOR of each class;
+then a random loss pattern -- uniform (every stripe loses 1..m data blocks in
+distinct classes), sparse (one stripe in ~9), skewed (a few stripes lose up to
+m, the rest nothing), or with lost parity blocks -- erased and rebuilt through
+every decode entry point and forced tiling.  A recoverable batch must come back
+bit-exact with parity untouched; one with an unrecoverable stripe must be left
+as erased (xec_decode_per_stripe: failing stripes only).
+
+    python tools/fuzz_big.py [--cases 60] [--seed 1] [--out f.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
+
+PATHS = ["auto", "stripe", "class", "list", "per_stripe", "device", "device_list"]
+
+
+def loss_pattern(np, rng, S, k, m, kind):
+    """Bitmap (S, k+m) uint8, 0 = lost."""
+    bm = np.ones((S, k + m), np.uint8)
+    nm = k // m
+    if kind == "uniform":
+        nlost = rng.integers(1, m + 1, size=S)
+    elif kind == "sparse":
+        nlost = np.where(rng.random(S) < 1 / 9, rng.integers(1, m + 1, size=S), 0)
+    else:  # skewed / parity
+        nlost = np.where(rng.random(S) < 0.05, m, 0) if kind == "skewed" else \
+            rng.integers(0, m + 1, size=S)
+    order = np.argsort(rng.random((S, m)), axis=1)  # distinct classes per stripe
+    rows = np.arange(S)
+    for q in range(m):
+        sel = nlost > q
+        cls = order[:, q]
+        mem = rng.integers(0, nm, size=S)
+        bm[rows[sel], (cls + m * mem)[sel]] = 0
+    if kind == "parity":  # lose the parity of classes that lost no data block
+        data_lost_cls = np.zeros((S, m), bool)
+        for j in range(m):
+            data_lost_cls[:, j] = (bm[:, j:k:m] == 0).any(axis=1)
+        drop = (~data_lost_cls) & (rng.random((S, m)) < 0.3)
+        bm[:, k:][drop] = 0
+    return bm
+
+
+def recoverable(np, bm, k, m):
+    lost = bm == 0
+    ok = np.ones(bm.shape[0], bool)
+    for j in range(m):
+        ok &= (lost[:, j:k:m].sum(axis=1) + lost[:, k + j]) <= 1
+    return ok
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=60)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import xec
+
+    torch.cuda.set_device(0)
+    assert xec.init(0) == 0
+    s = torch.cuda.current_stream()
+    rng = np.random.default_rng(args.seed)
+    log = []
+    t_start = time.time()
+    for case in range(args.cases):
+        m = int(rng.choice([1, 1, 2, 4, 8, 3, 5]))
+        k = m * int(rng.integers(1, max(2, 64 // m) + 1))
+        bs = 256 * int(rng.choice([1, 3, 16, 64, 256, 1024, 4096]))
+        target = int(rng.integers(128 << 20, 2 << 30))
+        S = max(1, target // (k * bs))
+        kind = ["uniform", "sparse", "skewed", "parity"][case % 4]
+        unrec = case % 7 == 3  # one unrecoverable stripe
+        d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+        p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+        assert xec.fill_splitmix64(d, S, k * bs, 5000 + case, s) == 0
+        assert xec.encode(d, p, S, bs, k, m, s) == 0
+        # parity == XOR over each class (as bench.py verifies)
+        blocks = d.view(S, k // m, m, bs)
+        red = blocks[:, 0].clone()
+        for r in range(1, k // m):
+            red.bitwise_xor_(blocks[:, r])
+        enc_ok = bool(torch.equal(red.reshape(-1), p))
+        del red, blocks
+        orig_d = d.clone()
+        orig_p = p.clone()
+        bm = loss_pattern(np, rng, S, k, m, kind)
+        if unrec:
+            c = int(rng.integers(0, S))
+            bm[c, :] = 1
+            bm[c, 0] = 0
+            bm[c, k] = 0
+        rec = recoverable(np, bm, k, m)
+        h_bm = torch.from_numpy(bm.reshape(-1).copy()).pin_memory()
+        d_bm = h_bm.to("cuda")
+        rec_t = torch.from_numpy(rec).to("cuda")
+        results = {}
+        for path in PATHS:
+            d.copy_(orig_d)
+            p.copy_(orig_p)
+            assert xec.erase(d, p, S, bs, k, m, d_bm, s) == 0
+            erased = d.clone()
+            erased_p = p.clone()
+            scratch = torch.empty_like(d_bm)
+            if path in ("auto", "stripe", "class", "list"):
+                xec.set_decode_tiling({"auto": 0, "stripe": 1, "class": 2, "list": 3}[path])
+                st = int(xec.decode(d, p, S, bs, k, m, h_bm, scratch, s))
+                xec.set_decode_tiling(0)
+            elif path == "per_stripe":
+                st = int(xec.decode_per_stripe(d, p, S, bs, k, m, h_bm, scratch, None, s))
+            else:
+                dst = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+                if path == "device":
+                    assert xec.decode_device(d, p, S, bs, k, m, d_bm, dst, s) == 0
+                    torch.cuda.synchronize()
+                    st = int(dst.item())
+                else:
+                    n = xec.device_list_bytes(S, k, m)
+                    w = torch.empty((n + 3) // 4, dtype=torch.int32, device="cuda")
+                    st = int(xec.decode_device_list(d, p, S, bs, k, m, d_bm, w, n, dst, s))
+                    if st == 0:
+                        torch.cuda.synchronize()
+                        st = int(dst.item())
+                    del w
+            torch.cuda.synchronize()
+            par_ok = bool(torch.equal(p, erased_p))
+            if k > 256 and path in ("per_stripe", "device_list"):
+                ok = st == 1 and bool(torch.equal(d, erased))
+            elif path == "per_stripe":
+                want = torch.where(rec_t[:, None], orig_d.view(S, -1), erased.view(S, -1))
+                ok = st == (0 if rec.all() else 4) and bool(torch.equal(d.view(S, -1), want))
+                del want
+            elif rec.all():
+                ok = st == 0 and bool(torch.equal(d, orig_d))
+            else:
+                ok = st == 4 and bool(torch.equal(d, erased))
+            results[path] = bool(ok and par_ok)
+            del erased, erased_p
+        row = {"case": case, "k": k, "m": m, "bs": bs, "S": S, "GiB": round(S * k * bs / 2**30, 3),
+               "pattern": kind, "lost_data_blocks": int((bm[:, :k] == 0).sum()),
+               "recoverable": bool(rec.all()), "encode_ok": enc_ok, "decode_ok": results}
+        log.append(row)
+        bad = (not enc_ok) or not all(results.values())
+        print(("FAIL " if bad else "ok   ") + json.dumps(row), flush=True)
+        del d, p, orig_d, orig_p, d_bm, h_bm, rec_t
+        torch.cuda.empty_cache()
+        if bad:
+            break
+    n_ok = sum(1 for r in log if r["encode_ok"] and all(r["decode_ok"].values()))
+    summary = {"cases": len(log), "all_ok": n_ok == len(log), "seconds": round(time.time() - t_start, 1)}
+    print(json.dumps(summary), flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps({"summary": summary, "cases": log}, indent=1))
+    sys.exit(0 if summary["all_ok"] else 1)
+
+
+if __name__ == "__main__":
+    main()
