@@ -11,6 +11,13 @@ bit-exact with parity untouched; one with an unrecoverable stripe must be left
 as erased (xec_decode_per_stripe: failing stripes only).
 
     python tools/fuzz_big.py [--cases 60] [--seed 1] [--out f.json]
+    python tools/fuzz_big.py --pipeline ...   # the host-in/host-out pipeline instead
+
+--pipeline: the batch lives in pinned host memory (32-512 MiB); xec_pipeline
+encode must give the device encode's parity, and decode must restore the
+erased host batch (only classes that lost a data block travel at >= 64 KiB
+blocks, csrc/xec_pipeline.cpp), or leave it untouched when a stripe is
+unrecoverable.
 """
 from __future__ import annotations
 
@@ -65,6 +72,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=60)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--pipeline", action="store_true")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -77,6 +85,8 @@ def main():
     assert xec.init(0) == 0
     s = torch.cuda.current_stream()
     rng = np.random.default_rng(args.seed)
+    if args.pipeline:
+        return pipeline_fuzz(args, np, torch, xec, s, rng)
     log = []
     t_start = time.time()
     for case in range(args.cases):
@@ -163,6 +173,65 @@ def main():
         if bad:
             break
     n_ok = sum(1 for r in log if r["encode_ok"] and all(r["decode_ok"].values()))
+    summary = {"cases": len(log), "all_ok": n_ok == len(log), "seconds": round(time.time() - t_start, 1)}
+    print(json.dumps(summary), flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps({"summary": summary, "cases": log}, indent=1))
+    sys.exit(0 if summary["all_ok"] else 1)
+
+
+def pipeline_fuzz(args, np, torch, xec, s, rng):
+    log = []
+    t_start = time.time()
+    for case in range(args.cases):
+        m = int(rng.choice([1, 1, 2, 4, 8, 3]))
+        k = m * int(rng.integers(1, max(2, 32 // m) + 1))
+        bs = 256 * int(rng.choice([1, 16, 64, 256, 1024, 4096]))
+        target = int(rng.integers(32 << 20, 512 << 20))
+        S = max(1, target // (k * bs))
+        chunk = int(rng.integers(1, 17))
+        ns = int(rng.integers(1, 5))
+        kind = ["uniform", "sparse", "skewed", "parity"][case % 4]
+        unrec = case % 7 == 3
+        d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+        p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+        assert xec.fill_splitmix64(d, S, k * bs, 9000 + case, s) == 0
+        assert xec.encode(d, p, S, bs, k, m, s) == 0
+        h_d = torch.empty(S * k * bs, dtype=torch.uint8).pin_memory()
+        h_p = torch.empty(S * m * bs, dtype=torch.uint8).pin_memory()
+        h_d.copy_(d)
+        ref_p = p.cpu()
+        ref_d = h_d.clone()
+        del d, p
+        bm = loss_pattern(np, rng, S, k, m, kind)
+        if unrec:
+            c = int(rng.integers(0, S))
+            bm[c, :] = 1
+            bm[c, 0] = 0
+            bm[c, k] = 0
+        rec = recoverable(np, bm, k, m)
+        h_bm = torch.from_numpy(bm.reshape(-1).copy()).pin_memory()
+        with xec.Pipeline(chunk, bs, k, m, ns) as pl:
+            h_p.zero_()
+            enc_ok = pl.encode(h_d, h_p, S) == 0 and bool(torch.equal(h_p, ref_p))
+            hv = h_d.numpy().reshape(S, k, bs)
+            hv[bm[:, :k] == 0] = 0
+            erased = h_d.clone()
+            st = int(pl.decode(h_d, h_p, S, h_bm))
+        if rec.all():
+            dec_ok = st == 0 and bool(torch.equal(h_d, ref_d))
+        else:
+            dec_ok = st == 4 and bool(torch.equal(h_d, erased))
+        row = {"case": case, "k": k, "m": m, "bs": bs, "S": S, "chunk": chunk, "streams": ns,
+               "MiB": round(S * k * bs / 2**20, 1), "pattern": kind,
+               "recoverable": bool(rec.all()), "encode_ok": enc_ok, "decode_ok": dec_ok}
+        log.append(row)
+        bad = not (enc_ok and dec_ok)
+        print(("FAIL " if bad else "ok   ") + json.dumps(row), flush=True)
+        del h_d, h_p, ref_d, ref_p, erased, h_bm
+        if bad:
+            break
+    n_ok = sum(1 for r in log if r["encode_ok"] and r["decode_ok"])
     summary = {"cases": len(log), "all_ok": n_ok == len(log), "seconds": round(time.time() - t_start, 1)}
     print(json.dumps(summary), flush=True)
     if args.out:
