@@ -164,6 +164,23 @@ def test_multi_device_scatter_gather():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prog,ok", [("asan_multi_equiv", "multi_equiv ok"),
+                                     ("asan_multi_scatter", "multi_scatter ok")])
+def test_plugins_under_asan(prog, ok):
+    """Both plugins' host code (buffers, shards, per-shard decode threads, peer
+    copies) under AddressSanitizer on the GPU box: the host side only is
+    instrumented (tests/host/Makefile bin/asan_*); any report fails the run."""
+    import os
+    exe = ROOT / "tests" / "host" / "bin" / prog
+    assert exe.exists(), "build with make -C tests/host"
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0:"
+                                        "abort_on_error=0:exitcode=23")
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0 and ok in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
+    assert "AddressSanitizer" not in p.stderr, p.stderr[-4000:]
+
+
+@pytest.mark.gpu
 def test_multi_device_rows_clean():
     """`-g xorec-hip,xorec-hip-multi --devices 0,0,0`: one clean row per
     algorithm, in -g order (get_benchmarks, benchmark_suite.cpp:279-311); the
