@@ -165,11 +165,15 @@ def test_multi_device_scatter_gather():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("prog,ok", [("asan_multi_equiv", "multi_equiv ok"),
-                                     ("asan_multi_scatter", "multi_scatter ok")])
+                                     ("asan_multi_scatter", "multi_scatter ok"),
+                                     ("asan_abi", "abi_asan ok")])
 def test_plugins_under_asan(prog, ok):
-    """Both plugins' host code (buffers, shards, per-shard decode threads, peer
-    copies) under AddressSanitizer on the GPU box: the host side only is
-    instrumented (tests/host/Makefile bin/asan_*); any report fails the run."""
+    """Host code under AddressSanitizer on the GPU box: both plugins (buffers,
+    shards, per-shard decode threads, peer copies) and the C ABI itself (scans,
+    work-list staging, kernel-argument lists, per-stripe decode, pipeline run
+    merging, over exact-size host buffers; tests/host/abi_asan.cpp).  The host
+    side only is instrumented (tests/host/Makefile bin/asan_*); any report
+    fails the run."""
     import os
     exe = ROOT / "tests" / "host" / "bin" / prog
     assert exe.exists(), "build with make -C tests/host"
