@@ -23,7 +23,7 @@ def _bench(*args, timeout=300):
                           text=True, timeout=timeout, cwd=ROOT)
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])  # 8: the driver's largest scaling run
 def test_launcher_plain_command(n):
     p = _bench("--gpus", str(n), "--rehearse-cpu", "--dist-backend", "gloo",
                "--workload", "8,2,4096,5", "--steps", "3", "--warmup", "1")
@@ -44,6 +44,26 @@ def test_launcher_plain_command(n):
     assert sc["bit_exact"] is True and sc["gathered_parity_bit_exact_vs_root_encode"] is True
     # max-over-ranks: the reported step time covers every rank's elapsed time
     assert out["ms_per_step"] * out["steps"] >= max(r["elapsed_ms"] for r in out["per_rank"]) - 1e-3
+
+
+def test_torchrun_launch_one_line():
+    """Launched the way the driver launches N > 1 (torch.distributed.run, one rank
+    per process, WORLD_SIZE set): still exactly one line on stdout."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "4", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), str(ROOT / "bench.py"), "--gpus", "4", "--rehearse-cpu",
+                        "--dist-backend", "gloo", "--workload", "8,2,4096,5", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["dist"]["ranks_seen"] == 4
+    assert out["dist"]["launcher"] == "external"
 
 
 def test_launcher_propagates_rank_failure():
