@@ -829,6 +829,10 @@ def run_rank(args):
     if out is not None:
         print(json.dumps(out), file=result_out, flush=True)
     if use_dist:
+        # the other ranks wait here while rank 0 writes its line, so nothing they
+        # log while tearing down can land inside it when stdout and stderr share
+        # one pipe
+        dist.barrier()
         dist.destroy_process_group()
     if bad:
         sys.exit("verification failed")
