@@ -1,0 +1,39 @@
+// hip_buffers.hpp -- the few HIP runtime calls the reference-side plugin makes
+// (allocation, copies, stream synchronise), behind plain C++ functions.
+//
+// Why a second translation unit: the reference's utils.hpp includes
+// <cuda_runtime.h> (utils.hpp:17), whose dim3 / vector types collide with
+// <hip/hip_runtime_api.h>'s in one translation unit.  xorec_hip_bm.cpp
+// therefore includes the reference headers and this file only; hip_buffers.cpp
+// includes the HIP runtime and no reference header.  In a reference tree that
+// has dropped CUDA, the two files can be merged.
+#ifndef XEC_INTEGRATION_HIP_BUFFERS_HPP
+#define XEC_INTEGRATION_HIP_BUFFERS_HPP
+
+#include <cstddef>
+#include <cstdint>
+
+#include "xec.h"  // hipStream_t (opaque)
+
+namespace xec_hip {
+
+// Allocations; nullptr on failure.  The free functions have the signature of
+// the reference's DeleterFunc<uint8_t> (utils.hpp:112-113), so they can own
+// AbstractBenchmark's m_data_buf / m_parity_buf / m_block_bitmap.
+uint8_t* alloc_device(size_t bytes);
+uint8_t* alloc_pinned(size_t bytes);
+void free_device(uint8_t* p);
+void free_pinned(uint8_t* p);
+
+// Stream-ordered copies and a synchronise; true on success.
+bool copy_to_device(void* dst, const void* src, size_t bytes, hipStream_t stream);
+bool copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t stream);
+bool synchronize(hipStream_t stream);
+
+// A non-blocking stream of the current device; nullptr on failure.
+hipStream_t create_stream();
+void destroy_stream(hipStream_t stream);
+
+}  // namespace xec_hip
+
+#endif  // XEC_INTEGRATION_HIP_BUFFERS_HPP
