@@ -22,14 +22,17 @@ namespace {
 
 std::atomic<bool> g_initialised{false};
 
-// Launch-shape overrides (xec_set_launch); 0 = default.
-std::atomic<int> g_unroll{0};
-std::atomic<int> g_max_grid{0};
-std::atomic<int> g_nt{0};
-std::atomic<int> g_threads{0};
-std::atomic<int> g_occupancy{0};  // xec_set_occupancy: waves per SIMD, 0 = automatic
-std::atomic<int> g_decode_tiling{0};  // xec_set_decode_tiling: 0 auto, 1 stripe, 2 class, 3 list
-thread_local int g_tiling_used = 0;   // xec_decode_tiling_used: this thread's last xec_decode
+// Tuning overrides (xec_set_launch, xec_set_occupancy, xec_set_decode_tiling);
+// 0 = default.  Per thread: an override applies to the calls its own thread
+// makes, so a tuning sweep on one thread never changes the kernels that
+// another thread (a ShardPool worker, a pipeline user) launches meanwhile.
+thread_local int g_unroll = 0;
+thread_local int g_max_grid = 0;
+thread_local int g_nt = 0;
+thread_local int g_threads = 0;
+thread_local int g_occupancy = 0;      // waves per SIMD, 0 = automatic
+thread_local int g_decode_tiling = 0;  // 0 auto, 1 stripe, 2 class, 3 list
+thread_local int g_tiling_used = 0;    // xec_decode_tiling_used: this thread's last xec_decode
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
@@ -98,7 +101,7 @@ int decode_auto_occupancy(uint64_t nm, uint64_t lost_data, uint64_t S) {
 // clearly below that (-6 % at 8+2 with one loss per stripe, 3x slower at
 // 16+8 with one).  With m == 1 the tilings coincide.
 bool use_class_tiles(uint64_t S, uint64_t m, uint64_t lost_data) {
-  const int t = g_decode_tiling.load(std::memory_order_relaxed);
+  const int t = g_decode_tiling;
   if (m <= 1 || t == 1) return false;
   if (t == 2) return true;
   return lost_data > S && 2 * lost_data >= S * m;  // automatic (0, or 3 without a list)
@@ -185,15 +188,15 @@ void stage_release(Staging* st, bool queued, hipStream_t stream) {
 // capped per member count (auto_occupancy).
 xec::LaunchShape launch_shape(size_t bs, int auto_w) {
   xec::LaunchShape ls;
-  const int t = g_threads.load(std::memory_order_relaxed);
+  const int t = g_threads;
   ls.threads = t == 256 ? 256 : 64;
-  const int u = g_unroll.load(std::memory_order_relaxed);
+  const int u = g_unroll;
   ls.unroll = (u == 1 || u == 2) ? u : 1;
-  const int g = g_max_grid.load(std::memory_order_relaxed);
+  const int g = g_max_grid;
   ls.max_grid = g > 0 ? (uint32_t)g : 0u;
   // nt stores address the block with a 32-bit buffer offset (xec_kernels.hip)
-  ls.nt = g_nt.load(std::memory_order_relaxed) != 2 && bs <= 0x7fffffffu;
-  int w = g_occupancy.load(std::memory_order_relaxed);
+  ls.nt = g_nt != 2 && bs <= 0x7fffffffu;
+  int w = g_occupancy;
   if (w == 0) w = (ls.threads == 64 && ls.unroll == 1) ? auto_w : 0;
   ls.lds_bytes = lds_for_occupancy(w, ls.threads);
   return ls;
@@ -289,7 +292,7 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   // tiles would run (no copy at all); class tiles keep dense multi-erasure
   // batches.  The list is built by a second, listing pass only
   // when it is used (the first pass costs ~1.1 ns per stripe).
-  const int tiling = g_decode_tiling.load(std::memory_order_relaxed);
+  const int tiling = g_decode_tiling;
   const bool listable =
       (tiling == 0 || tiling == 3) && k <= kWorkItemMaxK && S <= kWorkItemMaxStripes;
   const bool small = scan.lost_data <= xec::kArgItems;
@@ -421,7 +424,7 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
   // No host view of the bitmap: the loss count is unknown, so the tiling is
   // the stripe tiling with the single-erasure residency table unless
   // xec_set_decode_tiling(2) says every class lost a block.
-  const bool cls = m > 1 && g_decode_tiling.load(std::memory_order_relaxed) == 2;
+  const bool cls = m > 1 && g_decode_tiling == 2;
   const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   if (xec::launch_check(d_bitmap, g, d_status, stream) != hipSuccess) return XEC_DEVICE_ERROR;
@@ -516,22 +519,22 @@ xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_
   if (unroll != 0 && unroll != 1 && unroll != 2) return XEC_INVALID_SIZE;
   if (max_grid < 0 || cache_policy < 0 || cache_policy > 2) return XEC_INVALID_SIZE;
   if (block_threads != 0 && block_threads != 64 && block_threads != 256) return XEC_INVALID_SIZE;
-  g_threads.store(block_threads, std::memory_order_relaxed);
-  g_unroll.store(unroll, std::memory_order_relaxed);
-  g_max_grid.store(max_grid, std::memory_order_relaxed);
-  g_nt.store(cache_policy, std::memory_order_relaxed);
+  g_threads = block_threads;
+  g_unroll = unroll;
+  g_max_grid = max_grid;
+  g_nt = cache_policy;
   return XEC_SUCCESS;
 }
 
 xec_status xec_set_occupancy(int waves_per_simd) {
   if (waves_per_simd < 0 || waves_per_simd > 8) return XEC_INVALID_SIZE;
-  g_occupancy.store(waves_per_simd, std::memory_order_relaxed);
+  g_occupancy = waves_per_simd;
   return XEC_SUCCESS;
 }
 
 xec_status xec_set_decode_tiling(int tiling) {
   if (tiling < 0 || tiling > 3) return XEC_INVALID_SIZE;
-  g_decode_tiling.store(tiling, std::memory_order_relaxed);
+  g_decode_tiling = tiling;
   return XEC_SUCCESS;
 }
 

@@ -91,7 +91,7 @@ hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, c
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,
                        hipStream_t s);
 // xec_set_validate_kernel: 0 auto, 1 lane per block, 2 wave per block.
-extern int g_validate_mode;
+extern thread_local int g_validate_mode;
 hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t seed,
                           hipStream_t s);
 hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, uint32_t* d_bad,

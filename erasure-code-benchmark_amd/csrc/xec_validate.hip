@@ -390,7 +390,7 @@ struct PatternK {
 
 }  // namespace
 
-int g_validate_mode = 0;  // 0 auto, 1 lane per block, 2 wave per block (xec_set_validate_kernel)
+thread_local int g_validate_mode = 0;  // 0 auto, 1 lane, 2 grouped (xec_set_validate_kernel; per thread)
 
 hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t seed,
                           hipStream_t s) {

@@ -57,32 +57,44 @@ XorecBenchmarkHipMulti::XorecBenchmarkHipMulti(const BenchmarkConfig& config)
   // (xec.partition.stripe_range)
   const size_t n = devs.size(), base = m_chunks / n, extra = m_chunks % n;
   m_shards.resize(n);
-  for (size_t i = 0; i < n; ++i) {
-    Shard& s = m_shards[i];
-    s.device = devs[i];
-    s.first = i * base + std::min(i, extra);
-    s.count = base + (i < extra ? 1 : 0);
-    if (xec_init(s.device) != XEC_SUCCESS)
-      throw std::runtime_error("xec_init(" + std::to_string(s.device) + ") failed");
-    check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
-    s.data = device_buffer(s.count * m_chunk_data_size, "hipMalloc data");
-    s.parity = device_buffer(s.count * m_chunk_parity_size, "hipMalloc parity");
-    s.d_bitmap = device_buffer(s.count * m_chunk_tot_blocks, "hipMalloc bitmap");
-    s.d_erase = device_buffer(s.count * m_chunk_tot_blocks, "hipMalloc erase bitmap");
-    s.d_bad = device_buffer(sizeof(uint32_t), "hipMalloc bad counter");
+  try {
+    for (size_t i = 0; i < n; ++i) {
+      Shard& s = m_shards[i];
+      s.device = devs[i];
+      s.first = i * base + std::min(i, extra);
+      s.count = base + (i < extra ? 1 : 0);
+      if (xec_init(s.device) != XEC_SUCCESS)
+        throw std::runtime_error("xec_init(" + std::to_string(s.device) + ") failed");
+      check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+      s.data = device_buffer(s.count * m_chunk_data_size, "hipMalloc data");
+      s.parity = device_buffer(s.count * m_chunk_parity_size, "hipMalloc parity");
+      s.d_bitmap = device_buffer(s.count * m_chunk_tot_blocks, "hipMalloc bitmap");
+      s.d_erase = device_buffer(s.count * m_chunk_tot_blocks, "hipMalloc erase bitmap");
+      s.d_bad = device_buffer(sizeof(uint32_t), "hipMalloc bad counter");
+    }
+    m_pool = std::make_unique<ShardPool>(n);
+  } catch (...) {
+    // a throwing constructor runs no destructor: release the streams made so
+    // far here (the buffers go with m_shards)
+    destroy_streams();
+    throw;
   }
-  m_pool = std::make_unique<ShardPool>(n);
 }
 
-XorecBenchmarkHipMulti::~XorecBenchmarkHipMulti() noexcept {
-  const DeviceRestore restore;
-  m_pool.reset();  // join the workers before the streams they use go
+void XorecBenchmarkHipMulti::destroy_streams() noexcept {
   for (Shard& s : m_shards) {
     if (s.stream == nullptr) continue;
     (void)hipSetDevice(s.device);
     (void)hipStreamSynchronize(s.stream);
     (void)hipStreamDestroy(s.stream);
+    s.stream = nullptr;
   }
+}
+
+XorecBenchmarkHipMulti::~XorecBenchmarkHipMulti() noexcept {
+  const DeviceRestore restore;
+  m_pool.reset();  // join the workers before the streams they use go
+  destroy_streams();
   // device buffers are released by their deleters after this body
 }
 
@@ -125,14 +137,29 @@ int XorecBenchmarkHipMulti::encode() noexcept {
   return ok ? 0 : -1;
 }
 
-// Every shard decodes its slice of the host bitmap (xec_decode: host scan,
-// then the launch), each on its own thread (m_pool), so no device's launch
-// waits for another's scan; then every stream is waited for.  A shard with an
-// unrecoverable stripe fails alone -- the others are still rebuilt, as the
-// reference's GPU decode is all-or-nothing only per call (xorec_gpu_cmp.cu:75-81).
+// All-or-nothing over the WHOLE batch, like the one-device plugin and the
+// reference's GPU decode (xorec_gpu_cmp.cu:75-81): every shard first checks its
+// slice of the host bitmap (xec_check_bitmap, is_recoverable per stripe,
+// xorec_utils.hpp:160-175), each on its own thread (m_pool); if any stripe of
+// any shard is unrecoverable the call returns DecodeFailure with nothing
+// launched on any device, so the bytes after a failed decode do not depend on
+// the device count.  Then every shard decodes its slice (xec_decode: host
+// scan, then the launch), again one thread each, so no device's launch waits
+// for another's scan; then every stream is waited for.
 int XorecBenchmarkHipMulti::decode() noexcept {
   const size_t n = m_shards.size();
   std::vector<int> st(n, XEC_DEVICE_ERROR);
+  m_pool->run([&](size_t i) {
+    const Shard& s = m_shards[i];
+    int needs = 0;
+    st[i] = xec_check_bitmap(m_block_bitmap.get() + s.first * m_chunk_tot_blocks, s.count,
+                             m_chunk_data_blocks, m_chunk_parity_blocks, &needs);
+  });
+  for (int v : st)
+    if (v != XEC_SUCCESS) {
+      m_last_status = v;
+      return -1;
+    }
   m_pool->run([&](size_t i) {
     const Shard& s = m_shards[i];
     const DeviceRestore restore;

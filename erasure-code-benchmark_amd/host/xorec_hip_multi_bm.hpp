@@ -13,7 +13,8 @@
 // sit at the same offsets inside its device's slice as they would in one
 // buffer, validation payloads and erasure draws are seeded by the GLOBAL
 // block / stripe index, so a batch gives the same bytes and the same losses
-// on one device or on eight.  config.devices lists the devices (repeats
+// on one device or on eight; decode() is all-or-nothing over the whole batch,
+// so a failed decode leaves the same bytes too.  config.devices lists the devices (repeats
 // allowed: two slices on one device exercise the sharding on a one-GPU box);
 // empty = every visible device.
 #pragma once
@@ -84,6 +85,7 @@ class XorecBenchmarkHipMulti : public AbstractBenchmark {
   std::vector<Shard> m_shards;
   std::unique_ptr<ShardPool> m_pool;  // decode(): one thread per shard (shard_pool.hpp)
   bool enable_peer(int root) noexcept;
+  void destroy_streams() noexcept;  // synchronise and destroy every shard's stream
   int m_last_status = 0;
 };
 

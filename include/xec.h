@@ -185,15 +185,21 @@ xec_status xec_write_validation_pattern(void* d_data, size_t nblocks, size_t bs,
 xec_status xec_validate_blocks(const void* d_data, size_t nblocks, size_t bs, uint32_t* d_bad,
                                hipStream_t stream);
 
-/* Launch-shape override for tuning sweeps (process-wide, not thread-safe
- * against concurrent launches).  Each argument 0 = the measured default:
+/* Tuning overrides: xec_set_launch, xec_set_occupancy, xec_set_decode_tiling
+ * and xec_set_validate_kernel are PER THREAD -- an override applies to the
+ * calls the setting thread makes afterwards and to no other thread's, so a
+ * sweep on one thread cannot change the kernels another thread launches
+ * concurrently (a new thread starts at the defaults).  The defaults are the
+ * measured best; a plugin need not call any of them.
+ *
+ * Launch-shape override for tuning sweeps.  Each argument 0 = the measured default:
  *   unroll        16-byte granules per lane per class member: 1 or 2;
  *   max_grid      workgroups per launch (grid-stride beyond), 0 = one per tile;
  *   cache_policy  1 = non-temporal loads/stores (nt), 2 = default policy;
  *   block_threads workgroup size, 64 (one wave) or 256. */
 xec_status xec_set_launch(int unroll, int max_grid, int cache_policy, int block_threads);
 
-/* Residency of the encode/decode kernels (process-wide, like xec_set_launch):
+/* Residency of the encode/decode kernels (per thread, like xec_set_launch):
  * at most `waves_per_simd` (1..8; 8 = no cap) waves resident per SIMD,
  * enforced by reserving LDS per workgroup (the kernels use none).
  * 0 = automatic (the default): the cap measured fastest for the member count

@@ -19,9 +19,27 @@
 
 namespace {
 
+// Makes stripe c unrecoverable on the host bitmap: its first lost data block's
+// class also loses its parity (is_recoverable, xorec_utils.hpp:160-175).
+void spoil(uint8_t* bm, size_t c, size_t k, size_t m) {
+  uint8_t* row = bm + c * (k + m);
+  for (size_t i = 0; i < k; ++i)
+    if (!row[i]) {
+      row[k + i % m] = 0;
+      return;
+    }
+}
+
+class Multi : public xec::XorecBenchmarkHipMulti {
+ public:
+  using XorecBenchmarkHipMulti::XorecBenchmarkHipMulti;
+  void spoil_stripe(size_t c) { spoil(m_block_bitmap.get(), c, m_chunk_data_blocks, m_chunk_parity_blocks); }
+};
+
 class Single : public xec::XorecBenchmarkHip {
  public:
   using XorecBenchmarkHip::XorecBenchmarkHip;
+  void spoil_stripe(size_t c) { spoil(m_block_bitmap.get(), c, m_chunk_data_blocks, m_chunk_parity_blocks); }
   void read(std::vector<uint8_t>& d, std::vector<uint8_t>& p) const {
     d.resize(m_chunks * m_chunk_data_size);
     p.resize(m_chunks * m_chunk_parity_size);
@@ -40,7 +58,8 @@ void read_multi(const xec::XorecBenchmarkHipMulti& b, size_t kbs, size_t mbs,
       std::fprintf(stderr, "read_shard %zu failed\n", i);
 }
 
-int check(size_t S, size_t k, size_t m, size_t bs, size_t lost, std::vector<int> devices) {
+int check(size_t S, size_t k, size_t m, size_t bs, size_t lost, std::vector<int> devices,
+          bool unrecoverable = false) {
   xec::BenchmarkConfig c;
   c.message_size = S * k * bs;
   c.block_size = bs;
@@ -50,7 +69,7 @@ int check(size_t S, size_t k, size_t m, size_t bs, size_t lost, std::vector<int>
   c.seed = 5;
   c.devices = devices;
   Single one(c);
-  xec::XorecBenchmarkHipMulti multi(c);
+  Multi multi(c);
   if (multi.shards() != devices.size()) return 10;
   std::vector<uint8_t> d1, p1, dn, pn;
   int step = 0;
@@ -69,6 +88,15 @@ int check(size_t S, size_t k, size_t m, size_t bs, size_t lost, std::vector<int>
   multi.simulate_data_loss();
   if (!same(true)) return 3;
   if (lost > 0 && one.check_for_corruption()) return 4;  // the erasure must show
+  if (unrecoverable) {
+    // the LAST stripe (last shard) cannot be rebuilt: both plugins fail the
+    // whole batch and touch nothing, on one device or on several
+    one.spoil_stripe(S - 1);
+    multi.spoil_stripe(S - 1);
+    if (one.decode() == 0 || multi.decode() == 0) return 8;
+    if (!same(true)) return 9;
+    return 0;
+  }
   if (one.decode() != 0 || multi.decode() != 0) return 5;
   if (!same(false)) return 6;
   if (!one.check_for_corruption() || !multi.check_for_corruption()) return 7;
@@ -81,14 +109,17 @@ int main() {
   struct Case {
     size_t S, k, m, bs, lost;
     std::vector<int> devices;
+    bool unrecoverable = false;
   } cases[] = {
       {13, 8, 4, 4096, 3, {0, 0, 0}},      // uneven ranges: 5, 4, 4 stripes
       {7, 16, 1, 65536, 1, {0, 0}},        // 4 + 3
       {2, 32, 8, 1024, 8, {0, 0, 0, 0}},   // more shards than stripes: two empty
       {64, 16, 4, 8192, 0, {0}},           // one shard, nothing lost
+      {13, 8, 4, 4096, 2, {0, 0, 0}, true},  // last stripe unrecoverable: nothing rebuilt anywhere
+      {9, 16, 1, 8192, 1, {0, 0}, true},
   };
   for (const Case& x : cases) {
-    const int rc = check(x.S, x.k, x.m, x.bs, x.lost, x.devices);
+    const int rc = check(x.S, x.k, x.m, x.bs, x.lost, x.devices, x.unrecoverable);
     if (rc != 0) {
       std::printf("multi_equiv FAILED at S=%zu k=%zu m=%zu bs=%zu lost=%zu shards=%zu: %d\n", x.S,
                   x.k, x.m, x.bs, x.lost, x.devices.size(), rc);

@@ -3,6 +3,8 @@
 shape (reference binary when oracle/_ref was built, else the port)."""
 from __future__ import annotations
 
+import pytest
+
 import bench
 
 
@@ -33,6 +35,25 @@ def test_cpu_baseline_shape():
     assert out["by_workload"]["cfg2"]["value"] == out["value"]
     for w in out["by_workload"].values():
         assert w["value"] > 0 and w["single_thread"]["value"] > 0
+    # nproc threads (and OMP_NUM_THREADS when different), model named
+    import os
+    assert out["nproc"] == len(os.sched_getaffinity(0))
+    assert str(out["nproc"]) in out["by_threads"]
+    assert out["cores"] in (int(c) for c in out["by_threads"])
+    assert out["value"] == max(out["by_threads"].values())
+    assert "cpu_model" in out
+
+
+def test_cpu_baseline_times_both_thread_counts(monkeypatch):
+    """OMP_NUM_THREADS below nproc: both counts timed, the difference noted."""
+    import os
+    nproc = len(os.sched_getaffinity(0))
+    if nproc < 2:
+        pytest.skip("needs 2 CPUs")
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    out = bench.cpu_baseline("cfg2", 8, 1, 1 << 16, 1024, 0.2, sample_bytes=16 << 20)
+    assert set(out["by_threads"]) == {str(nproc), "1"}
+    assert out["omp_num_threads"] == 1 and "differ" in out["threads_note"]
 
 
 def test_erasure_pattern_is_recoverable_and_exact():

@@ -74,6 +74,23 @@ def test_launcher_propagates_rank_failure():
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
 
 
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_hung_leg_is_visible_in_exit_status(gpus):
+    """The legs' watchdog (--scatter-timeout) fires while the scatter leg runs:
+    rank 0 still prints exactly one line, carrying the leg's error, and the
+    command -- the bench.py launcher at N=2, the lone rank at N=1 -- exits 3."""
+    extra = ["--dist-world1"] if gpus == 1 else []
+    p = _bench("--gpus", str(gpus), *extra, "--rehearse-cpu", "--dist-backend", "gloo",
+               "--workload", "8,2,4096,5", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+               "--scatter-timeout", "0.01", timeout=180)
+    assert p.returncode == 3, (p.returncode, p.stderr[-3000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
+    out = json.loads(lines[0])
+    assert "timed out" in out["scatter"]["error"]
+    assert out["verified"] is True and out["value"] > 0
+
+
 def test_world1_process_group_rehearsal():
     """--dist-world1 opens a one-rank group and runs the collectives + scatter leg."""
     p = _bench("--rehearse-cpu", "--dist-backend", "gloo", "--dist-world1",

@@ -185,6 +185,23 @@ def test_plugins_under_asan(prog, ok):
 
 
 @pytest.mark.gpu
+def test_overrides_per_thread_under_tsan():
+    """Tuning overrides are per thread (include/xec.h): three threads with
+    different xec_set_launch / xec_set_occupancy / xec_set_decode_tiling /
+    xec_set_validate_kernel settings run encode -> erase -> decode -> validate
+    concurrently, each sees only its own tiling and gets exact bytes, and the
+    C ABI's host code runs under ThreadSanitizer (tests/host/tsan_overrides.cpp;
+    host side only instrumented).  Any race report fails the run."""
+    import os
+    exe = ROOT / "tests" / "host" / "bin" / "tsan_overrides"
+    assert exe.exists(), "build with make -C tests/host"
+    env = dict(os.environ, TSAN_OPTIONS="exitcode=23:halt_on_error=0")
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert "ThreadSanitizer" not in p.stderr, p.stderr[-6000:]
+    assert p.returncode == 0 and "tsan_overrides ok" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
+
+
+@pytest.mark.gpu
 def test_multi_device_rows_clean():
     """`-g xorec-hip,xorec-hip-multi --devices 0,0,0`: one clean row per
     algorithm, in -g order (get_benchmarks, benchmark_suite.cpp:279-311); the

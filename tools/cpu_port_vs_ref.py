@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--out", default=str(ROOT / "profiles" / "r02_cpu_port_vs_ref.json"))
     a = ap.parse_args()
     o = xo.COracle()
-    threads_all = bench._host_threads()
+    threads_all = bench._host_threads()[0]  # nproc
     _, avx512 = bench._cpu_model()
     version = 3 if avx512 else 2
     rows = []

@@ -11,7 +11,10 @@ variant rebuilt the erased blocks bit-exactly (against a fresh device fill).
 Also times encode on the same buffers as the reference point.  Rates are
 algorithmic GB/s: decode (lost data blocks)*(k/m+1)*bs, encode S*(k+m)*bs per
 launch.  --pattern sparse keeps the losses of only every 9th stripe, skew only
-every 5th (the others lose nothing).
+every 5th (the others lose nothing); --pattern fraction keeps them on a
+fraction --fraction of the stripes, spread evenly over the batch (stripe c
+keeps its losses when frac(c * 0.618...) < f): the sweep that prices the
+work-list threshold (xec_api.cpp kListStripesNum / kListStripesDen).
 
     python tools/tiling_ab.py [--shapes 16,2,1048576,256:16,8,65536,16384]
                               [--pattern uniform|sparse|skew] [--out f.json]
@@ -44,7 +47,10 @@ def main():
                          "tiles at (variants class@oN); default: automatic residency only")
     ap.add_argument("--only-class", action="store_true",
                     help="time class tiles (and their --occ variants) and encode only")
-    ap.add_argument("--pattern", default="uniform", choices=["uniform", "sparse", "skew"])
+    ap.add_argument("--pattern", default="uniform",
+                    choices=["uniform", "sparse", "skew", "fraction"])
+    ap.add_argument("--fraction", default="0.5",
+                    help="--pattern fraction: comma list of stripe fractions that lose blocks")
     ap.add_argument("--variants", default="", help="comma list to keep (e.g. class,list)")
     ap.add_argument("--device", action="store_true",
                     help="also time the device-resident decodes: xec_decode_device (dev) and "
@@ -73,11 +79,16 @@ def main():
             assert xec.encode(d, p, S, bs, k, m, stream) == 0
             sets.append((d, p))
         b_enc, _ = algorithmic_bytes(S, k, m, bs)
-        for lost in losts:
+        fracs = ([float(x) for x in args.fraction.split(",")] if args.pattern == "fraction"
+                 else [None])
+        for lost, frac in ((lo, f) for lo in losts for f in fracs):
             if lost > m:
                 continue
             bm = erasure_pattern(np, S, k, m, lost)
-            if args.pattern != "uniform":
+            if args.pattern == "fraction":
+                keep = (np.arange(S) * 0.6180339887498949) % 1.0 < frac
+                bm[~keep] = 1
+            elif args.pattern != "uniform":
                 keep = np.arange(S) % (9 if args.pattern == "sparse" else 5) == 0
                 bm[~keep] = 1
             lost_blocks = int((bm[:, :k] == 0).sum())
@@ -149,6 +160,8 @@ def main():
             del fresh
             b_dec = lost_blocks * (k // m + 1) * bs
             row = {"k": k, "m": m, "bs": bs, "S": S, "pattern": args.pattern,
+                   "stripe_fraction": frac,
+                   "stripes_lost": int((bm[:, :k] == 0).any(axis=1).sum()),
                    "lost_per_stripe": lost, "lost_blocks": lost_blocks,
                    "class_fraction": lost / m, "bit_exact": ok}
             for v, ts in times.items():
