@@ -1,11 +1,13 @@
 """ROCTx ranges for profiling bench.py (rocprofv3), no effect otherwise.
 
-bench.py brackets its timed region with :func:`timed_region`: a ROCTx range
-named ``bench:timed`` (visible with ``rocprofv3 --marker-trace``) and
-``roctxProfilerResume`` / ``roctxProfilerPause``, so that
-``rocprofv3 --selected-regions --kernel-trace --stats`` profiles exactly the
-timed launches (tools/gpu_profile.sh).  The legs after the headline
-(host pipeline, scatter) get ranges of their own.  Without a profiler attached
+bench.py pauses the profiler first thing and brackets its timed region with
+:func:`timed_region`: ``roctxProfilerResume``, a ROCTx range named
+``bench:timed``, ``roctxProfilerPause``.  Under
+``rocprofv3 --marker-trace --kernel-trace --stats`` (tools/gpu_profile.sh) the
+control calls are honoured, so the kernel trace and its stats hold exactly the
+timed launches (ROCm 7.2, profiles/r03c: 5 of 11 probe launches traced; with
+``--selected-regions`` instead, nothing at all was recorded).  The legs after
+the headline (host pipeline, scatter) get ranges of their own.  Without a profiler attached
 the calls are no-ops inside the ROCTx library.  This is measurement plumbing,
 not the codec: when the ROCTx library is absent every function does nothing.
 """

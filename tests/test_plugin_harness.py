@@ -195,7 +195,8 @@ def test_overrides_per_thread_under_tsan():
     import os
     exe = ROOT / "tests" / "host" / "bin" / "tsan_overrides"
     assert exe.exists(), "build with make -C tests/host"
-    env = dict(os.environ, TSAN_OPTIONS="exitcode=23:halt_on_error=0")
+    supp = ROOT / "tests" / "host" / "tsan.supp"  # HSA-internal new/delete only
+    env = dict(os.environ, TSAN_OPTIONS=f"exitcode=23:halt_on_error=0:suppressions={supp}")
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
     assert "ThreadSanitizer" not in p.stderr, p.stderr[-6000:]
     assert p.returncode == 0 and "tsan_overrides ok" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]

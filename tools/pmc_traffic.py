@@ -65,9 +65,9 @@ def main():
         base = name.split("<")[0]
         if base not in algo:
             continue
-        # only the headline launches (default shape, one granule per lane): the
-        # bench's host-pipeline / scatter legs run two granules per lane
-        # (<NM, 2, ...>) on other batch sizes, so their bytes are not these
+        # only the default shape (one granule per lane); the PMC passes run
+        # without the bench's legs (tools/gpu_profile.sh), so every launch
+        # left is the headline batch
         targs = [a.strip() for a in name.split("<", 1)[1].rstrip(">").split(",")]
         if len(targs) > 1 and targs[1] != "1":
             continue

@@ -1,6 +1,6 @@
 # One GPU call's worth of round-end checks: GPU tests, smoke, default bench,
 # RCCL world-1 bench, and the default bench's kernel stats over the timed
-# region only (rocprofv3 --selected-regions: bench.py's markers.timed_region).
+# region only (rocprofv3 --marker-trace honours bench.py's markers.timed_region).
 set -o pipefail
 o=gpurun_out/${1:-r03}; mkdir -p $o
 export TMPDIR=/tmp
@@ -11,5 +11,5 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 tail -1 $o/smoke.txt
 timeout -k 10 300 python -u bench.py > $o/bench_default.log 2>&1 || { tail $o/bench_default.log; exit 1; }
 timeout -k 10 300 python -u bench.py --dist-world1 --no-cpu-baseline > $o/bench_world1_rccl.log 2>&1 || { tail $o/bench_world1_rccl.log; exit 1; }
-timeout -k 10 300 rocprofv3 --selected-regions --kernel-trace --stats -d $o/prof_timed -o kt --output-format csv -- python3 bench.py --no-cpu-baseline > $o/bench_prof_timed.log 2>&1 || { tail $o/bench_prof_timed.log; exit 1; }
+timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats -d $o/prof_timed -o kt --output-format csv -- python3 bench.py --no-cpu-baseline > $o/bench_prof_timed.log 2>&1 || { tail $o/bench_prof_timed.log; exit 1; }
 grep -o '"value": [0-9.]*' $o/bench_default.log $o/bench_world1_rccl.log
