@@ -8,8 +8,11 @@
 //   xec_bench -g xorec-hip[,xorec-hip-multi] [-f out.csv] [-a] [-i iters] [-w warmup]
 //             [-s simd,...] [-h]
 //
-//   -f, --file        output CSV (must contain ".csv"; default results.csv), written
-//                     at the given path (the reference prefixes ../results/raw/)
+//   -f, --file        output CSV (must contain ".csv"; default results.csv); a bare
+//                     file name lands in the raw-results directory, ../results/raw/
+//                     by default as in the reference (RAW_DIR + OUTPUT_FILE,
+//                     benchmark_suite.cpp:27,346, where scripts/utils/data.py
+//                     reads it); a path with a '/' is used as given
 //   -a, --append      append rows without a header (default: overwrite + header,
 //                     csv_reporter.cpp:11-19)
 //   -i, --iterations  timed iterations per config (> 0, default 10)
@@ -36,6 +39,8 @@
 //   --sync MODE      hipSetDeviceFlags: 0 default, 1 spin, 2 yield, 3 blocking
 //   --host-validation  payload written/checked on the host + copies, as the reference
 //   --stdout         CSV to stdout instead of -f
+//   --raw-dir DIR    directory for a bare -f name (default ../results/raw/; created
+//                    if missing; "" = the working directory)
 #include <getopt.h>
 #include <omp.h>
 
@@ -44,6 +49,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <filesystem>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -98,7 +104,7 @@ void usage() {
       "  -h, --help\n"
       "extensions: --message B --block B --data K --parity M --lost L | --sweep FILE\n"
       "            --threads N --device D --devices LIST --seed S --sync MODE\n"
-      "            --host-validation --stdout\n"
+      "            --host-validation --stdout --raw-dir DIR\n"
       "without config options -g runs the reference's GPU sweep (get_gpu_configs)\n");
 }
 
@@ -137,7 +143,7 @@ std::vector<xec::BenchmarkConfig> gpu_sweep(const xec::BenchmarkConfig& base) {
 
 int main(int argc, char** argv) {
   enum { kMessage = 1000, kBlock, kData, kParity, kLost, kSweep, kThreads, kDevice, kSeed, kSync,
-         kHostVal, kStdout, kDevices };
+         kHostVal, kStdout, kDevices, kRawDir };
   const option long_options[] = {
       {"help", no_argument, nullptr, 'h'},
       {"file", required_argument, nullptr, 'f'},
@@ -160,6 +166,7 @@ int main(int argc, char** argv) {
       {"host-validation", no_argument, nullptr, kHostVal},
       {"stdout", no_argument, nullptr, kStdout},
       {"devices", required_argument, nullptr, kDevices},
+      {"raw-dir", required_argument, nullptr, kRawDir},
       {nullptr, 0, nullptr, 0}};
 
   xec::BenchmarkConfig base;
@@ -179,6 +186,7 @@ int main(int argc, char** argv) {
   bool single_mode = false, overwrite = true, to_stdout = false;
   std::vector<std::string> algorithms;  // selected GPU algorithms, in -g order
   std::string out_file = "results.csv", sweep;
+  std::string raw_dir = "../results/raw/";  // RAW_DIR, benchmark_suite.cpp:27
 
   int c, idx = 0;
   while ((c = getopt_long(argc, argv, "hf:ai:w:c:g:s:", long_options, &idx)) != -1) {
@@ -225,6 +233,7 @@ int main(int argc, char** argv) {
       case kSync: base.sync_mode = std::atoi(optarg); break;
       case kHostVal: base.host_validation = true; break;
       case kStdout: to_stdout = true; break;
+      case kRawDir: raw_dir = optarg; break;
       case kDevices:
         base.devices.clear();
         for (const auto& d : arg_vector(optarg)) {
@@ -284,8 +293,15 @@ int main(int argc, char** argv) {
     std::ofstream f;
     std::ostream* os = &std::cout;
     if (!to_stdout) {
-      f.open(out_file, overwrite ? std::ios::out : std::ios::app);
-      if (!f.is_open()) fail("Error opening file: " + out_file);
+      // a bare name goes to the raw-results directory (benchmark_suite.cpp:346)
+      std::string path = out_file;
+      if (out_file.find('/') == std::string::npos && !raw_dir.empty()) {
+        std::error_code ec;
+        std::filesystem::create_directories(raw_dir, ec);
+        path = (std::filesystem::path(raw_dir) / out_file).string();
+      }
+      f.open(path, overwrite ? std::ios::out : std::ios::app);
+      if (!f.is_open()) fail("Error opening file: " + path);
       os = &f;
     }
     // CSVReporter (csv_reporter.cpp:11-19): header only when overwriting

@@ -65,6 +65,25 @@ def test_cli_contract_errors():
     assert r.returncode == 1 and "Invalid device" in r.stderr
 
 
+def test_csv_location_contract(tmp_path):
+    """A bare -f name lands in ../results/raw/ as in the reference (RAW_DIR +
+    OUTPUT_FILE, benchmark_suite.cpp:27,346; scripts/utils/data.py reads it
+    there); --raw-dir moves it; a path with '/' is used as given.  The CSV is
+    opened, with its header, before any device work, so this runs on the CPU
+    (the run itself then stops at xec_init without a GPU)."""
+    cwd = tmp_path / "a" / "b"
+    cwd.mkdir(parents=True)
+    cfg = ("--message", "8M", "--block", "4K", "--data", "8", "--parity", "1", "--lost", "0",
+           "-i", "1")
+    run("-g", "xorec-hip", "-f", "bare.csv", *cfg, cwd=cwd, timeout=120)
+    assert (tmp_path / "a" / "results" / "raw" / "bare.csv").read_text().startswith("name,err_msg")
+    run("-g", "xorec-hip", "-f", "moved.csv", "--raw-dir", str(tmp_path / "r"), *cfg, cwd=cwd,
+        timeout=120)
+    assert (tmp_path / "r" / "moved.csv").exists()
+    run("-g", "xorec-hip", "-f", "./here.csv", *cfg, cwd=cwd, timeout=120)
+    assert (cwd / "here.csv").exists()
+
+
 @pytest.mark.gpu
 def test_reference_gpu_sweep(tmp_path):
     """`xec_bench -g xorec-hip -f out.csv -i 3`: one clean row per config of the

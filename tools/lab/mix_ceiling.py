@@ -12,6 +12,8 @@ stream):
   read    tools/lab/mix_kernels.hip MODE 0: only the decode's reads
   write   MODE 1: only the decode's rebuilt-block writes
   lab     MODE 2: the lab's restatement of the decode (fidelity check)
+  spread  MODE 3: the same, tiles walked list-entry-fastest (many rebuilt
+          blocks written at once instead of the product's few)
   encode  the product's encode of the same batch (reference point)
 all at the product's residency for k/m (xec_api.cpp auto_occupancy).  The mix
 ceiling is the two streams one after the other: t_read + t_write for the
@@ -99,11 +101,11 @@ def main():
                 return xec.encode(d, p, S, bs, k, m, stream)
             if v in ("decode", "auto"):
                 return xec.decode(d, p, S, bs, k, m, h_bm, scratch[i % 3], stream)
-            mode = {"read": 0, "write": 1, "lab": 2}[v]
+            mode = {"read": 0, "write": 1, "lab": 2, "spread": 3}[v]
             return L.mix_launch(mode, d.data_ptr(), p.data_ptr(), items.data_ptr(), n_items,
                                 k, m, bs, lds, sp)
 
-        variants = ["decode", "auto", "read", "write", "lab", "encode"]
+        variants = ["decode", "auto", "read", "write", "lab", "spread", "encode"]
         times = {v: [] for v in variants}
         it = 0
         for _ in range(args.rounds):
@@ -140,6 +142,7 @@ def main():
                "decode_TBps": round(b_dec / med["decode"] / 1e9, 3),
                "auto_TBps": round(b_dec / med["auto"] / 1e9, 3),
                "lab_TBps": round(b_dec / med["lab"] / 1e9, 3),
+               "spread_TBps": round(b_dec / med["spread"] / 1e9, 3),
                "encode_TBps": round(b_enc / med["encode"] / 1e9, 3),
                "mix_ceiling_TBps": round(b_dec / ceiling_ms / 1e9, 3),
                "decode_over_ceiling": round(ceiling_ms / med["decode"], 4),

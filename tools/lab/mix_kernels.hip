@@ -10,7 +10,10 @@
 //           four words, which random data never does (the loads stay live);
 //   MODE 1  writes only: the rebuilt-block store, a value computed from the
 //           address (no loads);
-//   MODE 2  both: the product's decode, restated (fidelity check of the lab).
+//   MODE 2  both: the product's decode, restated (fidelity check of the lab);
+//   MODE 3  both, tiles walked entry-fastest (tile t -> entry t mod n, chunk
+//           t / n): concurrent workgroups spread over many rebuilt blocks
+//           instead of the product's few (destination order the other way round).
 // So MODE 0 / MODE 1 time the decode's exact read and write streams on their
 // own, and their sum is the time the two take one after the other.
 #include <hip/hip_runtime.h>
@@ -37,8 +40,10 @@ __global__ __launch_bounds__(64) void mix_kernel(uint8_t* data, const uint8_t* _
   const uint64_t stride = g.m * g.bs;
   for (uint64_t t0 = blockIdx.x; t0 < g.total_tiles; t0 += gridDim.x) {
     const uint64_t t = g.total_tiles - 1 - t0;
-    const uint32_t item = *(const_u32_as4)(items + t / g.tiles_per_block);
-    const uint64_t chunk = t % g.tiles_per_block;
+    const uint64_t n = g.total_tiles / g.tiles_per_block;
+    const uint64_t e = MODE == 3 ? t % n : t / g.tiles_per_block;
+    const uint32_t item = *(const_u32_as4)(items + e);
+    const uint64_t chunk = MODE == 3 ? t / n : t % g.tiles_per_block;
     const uint64_t c = item >> 8;
     const uint32_t i = item & 0xFFu;
     const uint32_t j = i % (uint32_t)g.m, r = i / (uint32_t)g.m;
@@ -77,7 +82,8 @@ hipError_t launch_nm(int mode, uint8_t* d, const uint8_t* p, const uint32_t* ite
                      uint32_t grid, uint32_t lds, hipStream_t s) {
   if (mode == 0) mix_kernel<NM, 0><<<grid, 64, lds, s>>>(d, p, items, g, 0x9E3779B9u);
   else if (mode == 1) mix_kernel<NM, 1><<<grid, 64, lds, s>>>(d, p, items, g, 0x9E3779B9u);
-  else mix_kernel<NM, 2><<<grid, 64, lds, s>>>(d, p, items, g, 0x9E3779B9u);
+  else if (mode == 2) mix_kernel<NM, 2><<<grid, 64, lds, s>>>(d, p, items, g, 0x9E3779B9u);
+  else mix_kernel<NM, 3><<<grid, 64, lds, s>>>(d, p, items, g, 0x9E3779B9u);
   return hipGetLastError();
 }
 
