@@ -5,13 +5,15 @@
 //   - argument checks                xorec_utils.hpp:61-86
 //   - batch recoverability scan      xorec_gpu_cmp.cu:75-81 (require_recovery /
 //                                    is_recoverable, xorec_utils.hpp:144-175)
-//   - stream-ordered H2D bitmap copy xorec_gpu_cmp.cu:83
+//   - H2D bitmap / work-list upload  xorec_gpu_cmp.cu:83 (here off the caller's
+//                                    stream, upload_begin below)
 // then one kernel launch per call (xec_kernels.hip).
 #include "xec.h"
 
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -181,6 +183,147 @@ void stage_release(Staging* st, bool queued, hipStream_t stream) {
   st->busy = false;
 }
 
+// ---- uploads off the caller's stream ---------------------------------------
+// What a decode kernel reads besides the batch -- the bitmap or the work list
+// -- comes from host memory.  Copied on the caller's stream, the copy waits
+// for the kernel before it and the decode kernel for the copy (the copy
+// engine's start and completion hand-offs included): 17-73 us per decode in
+// tools/lab/mix_ceiling.py (profiles/r03f: event time minus kernel time at
+// 16+8, 32+8, 32+1 x 4 KiB), 2-8 % of those decodes.  So the bytes go to a
+// device buffer the library owns, on a copy stream of its own (one per
+// device, non-blocking), which starts at once -- while the caller's stream is
+// still busy with earlier work -- and the decode kernel only waits for the
+// copy's event.  A buffer is reused once the kernel that read it has passed
+// (its event on the caller's stream); buffers are kept for the life of the
+// process, at most kMaxSlots per device unless every one is in use.  The
+// caller's d_bitmap scratch is used instead when no buffer can be had.
+struct DevSlot {
+  void* dev = nullptr;
+  size_t cap = 0;
+  int device = -1;
+  hipEvent_t copied = nullptr;  // on the copy stream, after the upload
+  hipEvent_t done = nullptr;    // on the caller's stream, after the reading kernel
+  bool busy = false;
+};
+constexpr size_t kMaxSlots = 16;
+std::mutex g_slot_mu;
+std::vector<DevSlot*> g_slots;
+std::vector<std::pair<int, hipStream_t>> g_copy_streams;
+
+hipStream_t copy_stream(int dev) {  // under g_slot_mu
+  for (auto& cs : g_copy_streams)
+    if (cs.first == dev) return cs.second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  g_copy_streams.emplace_back(dev, s);
+  return s;
+}
+
+struct Upload {
+  DevSlot* slot = nullptr;  // null: the bytes went to the caller's scratch on `stream`
+  hipStream_t cs = nullptr;  // the copy stream they went on
+  uint8_t* dev = nullptr;   // where the kernel reads them
+};
+
+// XEC_SCRATCH_UPLOADS=1 in the environment sends every upload through the
+// caller's scratch on the stream (the fallback path; tests use it).
+bool side_uploads() {
+  static const bool off = [] {
+    const char* e = std::getenv("XEC_SCRATCH_UPLOADS");
+    return e != nullptr && e[0] == '1';
+  }();
+  return !off;
+}
+
+bool capturing(hipStream_t stream) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(stream, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
+}
+
+// Starts copying `bytes` of host memory to a library buffer on the device's
+// copy stream; false (nothing queued) if no buffer or stream can be had.
+bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
+  DevSlot* pick = nullptr;
+  hipStream_t cs = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    cs = copy_stream(dev);
+    if (cs == nullptr) return false;
+    for (DevSlot* sl : g_slots) {
+      if (sl->busy || sl->device != dev || sl->cap < bytes) continue;
+      if (hipEventQuery(sl->done) != hipSuccess) continue;  // a kernel still reads it
+      if (pick == nullptr || sl->cap < pick->cap) pick = sl;
+    }
+    size_t mine = 0;
+    for (DevSlot* sl : g_slots) mine += sl->device == dev;
+    if (pick == nullptr && mine >= kMaxSlots) {
+      for (DevSlot* sl : g_slots)  // recycle an idle one: wait for its reader
+        if (!sl->busy && sl->device == dev) {
+          pick = sl;
+          break;
+        }
+      if (pick == nullptr) return false;
+      if (hipEventSynchronize(pick->done) != hipSuccess) return false;
+      if (pick->cap < bytes) {
+        (void)hipFree(pick->dev);
+        pick->dev = nullptr;
+        pick->cap = 0;
+      }
+    }
+    if (pick == nullptr) {
+      pick = new DevSlot;
+      pick->device = dev;
+      if (hipEventCreateWithFlags(&pick->copied, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {
+        if (pick->copied) (void)hipEventDestroy(pick->copied);
+        delete pick;
+        return false;
+      }
+      g_slots.push_back(pick);
+    }
+    pick->busy = true;
+  }
+  if (pick->cap < bytes) {
+    size_t cap = 64u << 10;
+    while (cap < bytes) cap <<= 1;
+    if (hipMalloc(&pick->dev, cap) != hipSuccess) {
+      pick->dev = nullptr;
+      pick->cap = 0;
+      std::lock_guard<std::mutex> lk(g_slot_mu);
+      pick->busy = false;
+      return false;
+    }
+    pick->cap = cap;
+  }
+  if (hipMemcpyAsync(pick->dev, host, bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
+      hipEventRecord(pick->copied, cs) != hipSuccess) {
+    (void)hipStreamSynchronize(cs);
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    pick->busy = false;
+    return false;
+  }
+  up.slot = pick;
+  up.cs = cs;
+  up.dev = static_cast<uint8_t*>(pick->dev);
+  return true;
+}
+
+// The caller's stream waits for the upload (before the kernel that reads it).
+bool upload_join(const Upload& up, hipStream_t stream) {
+  return up.slot == nullptr || hipStreamWaitEvent(stream, up.slot->copied, 0) == hipSuccess;
+}
+
+// After the launch (`launched`: a kernel on `stream` reads the buffer) or
+// without one: the buffer is free once that kernel, or the copy, has passed.
+void upload_end(Upload& up, hipStream_t stream, bool launched) {
+  if (up.slot == nullptr) return;
+  hipStream_t after = launched ? stream : up.cs;
+  if (hipEventRecord(up.slot->done, after) != hipSuccess) (void)hipStreamSynchronize(after);
+  std::lock_guard<std::mutex> lk(g_slot_mu);
+  up.slot->busy = false;
+  up.slot = nullptr;
+}
+
 // Defaults measured on MI355X (tools/sweep.py, profiles/r01_sweep_*.json):
 // non-temporal loads and parity stores, sc1 rebuilt-block stores (every byte
 // is touched once; xec_kernels.hip kEncodeStoreAux / kDecodeStoreAux), one-wave
@@ -278,15 +421,32 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
+  // The host scan reads h_bitmap now: a graph captured from this call would
+  // replay this call's losses whatever the bitmap holds then.  Refused before
+  // anything is queued; xec_decode_device is the capturable form.
+  if (capturing(stream)) return XEC_DEVICE_ERROR;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
+  const bool side = side_uploads();
   const size_t bitmap_bytes = S * (k + m);
+  // The bitmap goes to the device (a library buffer, or the caller's scratch
+  // on `stream`); for large bitmaps before the scan, so the two overlap.
+  Upload bmu;
+  auto upload_bitmap = [&]() -> bool {
+    if (side && upload_begin(h_bitmap, bitmap_bytes, dev, bmu)) return true;
+    bmu = Upload{};
+    bmu.dev = d_bitmap;
+    return hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice, stream) ==
+           hipSuccess;
+  };
   const bool copy_first = bitmap_bytes >= kCopyFirstBitmapBytes;
-  if (copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
-                                   stream) != hipSuccess)
-    return XEC_DEVICE_ERROR;
+  if (copy_first && !upload_bitmap()) return XEC_DEVICE_ERROR;
   XecScan scan;
   st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
-  if (st != XEC_SUCCESS) return st;  // nothing but the scratch copy was queued
-  if (!scan.needs_recovery || scan.lost_data == 0) return XEC_SUCCESS;  // nothing to rebuild
+  if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) {
+    upload_end(bmu, stream, false);  // only the bitmap copy was queued, if anything
+    return st;                       // failure, or nothing to rebuild
+  }
   // Which tiling: list tiles when the losses are sparse (or forced); for a
   // list short enough to travel in the kernel arguments also wherever stripe
   // tiles would run (no copy at all); class tiles keep dense multi-erasure
@@ -303,6 +463,7 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
     const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
     const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
     if (small) {  // the launch copies the list into its kernel arguments
+      upload_end(bmu, stream, false);
       uint32_t items[xec::kArgItems];
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, items, xec::kArgItems);
       if (st != XEC_SUCCESS) return st;
@@ -312,48 +473,60 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
                  ? XEC_SUCCESS
                  : XEC_DEVICE_ERROR;
     }
-    // Device list: u32 entries in the 4-byte-aligned part of the caller's
-    // S*(k+m)-byte scratch, staged in pinned host memory by the listing pass.
+    // u32 entries staged in pinned host memory by the listing pass, then
+    // uploaded: to a library buffer off the stream, or into the 4-byte-aligned
+    // part of the caller's S*(k+m)-byte scratch on it (if the list fits)
     const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
     const uint64_t cap = bitmap_bytes > pad ? (bitmap_bytes - pad) / 4 : 0;
-    int dev = 0;
+    const uint64_t n = scan.lost_data;
     Staging* sg = nullptr;
-    if (scan.lost_data <= cap && hipGetDevice(&dev) == hipSuccess)
-      sg = stage_acquire(scan.lost_data * 4, dev);
+    if (side || n <= cap) sg = stage_acquire(n * 4, dev);
     if (sg != nullptr) {
-      st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, static_cast<uint32_t*>(sg->host),
-                           scan.lost_data);
+      st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, static_cast<uint32_t*>(sg->host), n);
       if (st != XEC_SUCCESS) {
         stage_release(sg, false, stream);
+        upload_end(bmu, stream, false);
         return st;
       }
-      // stream-ordered after any bitmap copy into the same scratch
-      uint8_t* d_items = d_bitmap + pad;
-      const bool copied = hipMemcpyAsync(d_items, sg->host, scan.lost_data * 4,
-                                         hipMemcpyHostToDevice, stream) == hipSuccess;
-      stage_release(sg, copied, stream);
-      if (!copied) return XEC_DEVICE_ERROR;
-      g_tiling_used = XEC_TILING_LIST;
-      return xec::launch_decode(d_data, d_parity, d_items, g, ls, xec::kDecodeListTiles, stream,
-                                scan.lost_data) == hipSuccess
-                 ? XEC_SUCCESS
-                 : XEC_DEVICE_ERROR;
+      Upload lu;
+      bool ok = true;
+      if (side && upload_begin(sg->host, n * 4, dev, lu)) {
+        stage_release(sg, true, lu.cs);
+        ok = upload_join(lu, stream);
+      } else if (n <= cap) {
+        // stream-ordered after any bitmap copy into the same scratch
+        lu.dev = d_bitmap + pad;
+        ok = hipMemcpyAsync(lu.dev, sg->host, n * 4, hipMemcpyHostToDevice, stream) == hipSuccess;
+        stage_release(sg, ok, stream);
+      } else {
+        stage_release(sg, false, stream);  // denser than the scratch holds: bitmap tiles
+      }
+      if (lu.dev != nullptr) {
+        upload_end(bmu, stream, false);
+        g_tiling_used = XEC_TILING_LIST;
+        ok = ok && xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,
+                                      stream, n) == hipSuccess;
+        upload_end(lu, stream, true);
+        return ok ? XEC_SUCCESS : XEC_DEVICE_ERROR;
+      }
     }
-    // denser than the scratch holds as a list (or no staging memory): bitmap
+    // no staging memory, or a list denser than the scratch holds: bitmap tiles
   }
-  if (!copy_first && hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice,
-                                    stream) != hipSuccess)
+  if (!copy_first && !upload_bitmap()) return XEC_DEVICE_ERROR;
+  if (!upload_join(bmu, stream)) {
+    upload_end(bmu, stream, false);
     return XEC_DEVICE_ERROR;
+  }
   // class tiles: one reduction per tile, so the encode's residency table
   const xec::LaunchShape ls = launch_shape(
       bs, cls ? auto_occupancy(k / m) : decode_auto_occupancy(k / m, scan.lost_data, S));
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   g_tiling_used = cls && m > 1 ? XEC_TILING_CLASS : XEC_TILING_STRIPE;
-  return xec::launch_decode(d_data, d_parity, d_bitmap, g, ls,
-                            cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
-                            stream) == hipSuccess
-             ? XEC_SUCCESS
-             : XEC_DEVICE_ERROR;
+  const bool ok = xec::launch_decode(d_data, d_parity, bmu.dev, g, ls,
+                                     cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
+                                     stream) == hipSuccess;
+  upload_end(bmu, stream, true);
+  return ok ? XEC_SUCCESS : XEC_DEVICE_ERROR;
 }
 
 int xec_decode_tiling_used(void) { return g_tiling_used; }
@@ -367,6 +540,7 @@ xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, s
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
   if (k > kWorkItemMaxK || S > kWorkItemMaxStripes) return XEC_INVALID_SIZE;
+  if (capturing(stream)) return XEC_DEVICE_ERROR;  // host scan now: see xec_decode
   uint64_t n = 0, failures = 0;
   st = xec_scan_stripes(h_bitmap, S, k, m, h_codes, nullptr, 0, &n, &failures);
   if (st != XEC_SUCCESS) return st;
@@ -383,17 +557,28 @@ xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, s
                ? verdict
                : XEC_DEVICE_ERROR;
   }
-  // A longer list goes through the scratch in pieces of what it holds: copy
-  // a piece, rebuild it, copy the next (stream order keeps a copy behind the
-  // kernel still reading the previous piece).
-  const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
-  const uint64_t cap = (S * (k + m) - pad) / 4;  // >= 511 here: n > 1,024 <= S*k
+  // A longer list is uploaded whole off the stream (upload_begin), or else
+  // goes through the scratch in pieces of what it holds: copy a piece, rebuild
+  // it, copy the next (stream order keeps a copy behind the kernel still
+  // reading the previous piece).
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
   Staging* sg = stage_acquire(n * 4, dev);
   if (sg == nullptr) return XEC_DEVICE_ERROR;
   uint32_t* items = static_cast<uint32_t*>(sg->host);
   (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, n, &n, &failures);
+  g_tiling_used = XEC_TILING_LIST;
+  Upload lu;
+  if (side_uploads() && upload_begin(items, n * 4, dev, lu)) {
+    stage_release(sg, true, lu.cs);
+    const bool ok = upload_join(lu, stream) &&
+                    xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,
+                                       stream, n) == hipSuccess;
+    upload_end(lu, stream, true);
+    return ok ? verdict : XEC_DEVICE_ERROR;
+  }
+  const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
+  const uint64_t cap = (S * (k + m) - pad) / 4;  // >= 511 here: n > 1,024 <= S*k
   uint8_t* d_items = d_bitmap + pad;
   bool queued = false, ok = true;
   for (uint64_t q0 = 0; q0 < n && ok; q0 += cap) {
@@ -405,7 +590,6 @@ xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, s
                                   piece) == hipSuccess;
   }
   stage_release(sg, queued, stream);
-  g_tiling_used = XEC_TILING_LIST;
   return ok ? verdict : XEC_DEVICE_ERROR;
 }
 

@@ -72,19 +72,27 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * (require_recovery, xorec_utils.hpp:144-149).  Otherwise every lost data
  * block is rebuilt:
  *   data[c][i] = parity[c][i%m] ^ XOR_{l%m == i%m, l != i} data[c][l].
- * d_bitmap is scratch for the call: it may receive on `stream` a copy of
- * h_bitmap and/or the list of lost data blocks the host scan found (4 bytes
- * each).  The list drives one tile per lost block and 1 KiB chunk
- * (xec_set_decode_tiling); up to 1,024 entries travel in the kernel
- * arguments instead, and then nothing is copied.
+ * What the kernel reads besides the batch -- a copy of h_bitmap, or the list
+ * of lost data blocks the host scan found (4 bytes each; the list drives one
+ * tile per lost block and 1 KiB chunk, xec_set_decode_tiling) -- is copied to
+ * device buffers the library keeps, on a copy stream of its own that does not
+ * wait for `stream`'s earlier work; `stream` waits only for that copy before
+ * the decode kernel.  Up to 1,024 list entries travel in the kernel arguments
+ * instead, and then nothing is copied.  d_bitmap is scratch for the call,
+ * written on `stream` only when no library buffer can be had.  Not
+ * capturable: the host scan reads h_bitmap at call time, so a graph would
+ * replay this call's losses -- on a stream being captured the call returns
+ * XEC_DEVICE_ERROR with nothing queued (xec_decode_device is the capturable
+ * form).
  * Lost parity is not regenerated.  Parity is READ-ONLY here, as in the CPU
  * decode (xorec.cpp:62-111) -- deliberately unlike the reference GPU decode,
  * which folds all data into parity (xorec_gpu_cmp.cu:94-102).  The content of
  * lost data blocks on entry is irrelevant (no zeroing pre-condition).
- * The list is staged in pinned host memory the library keeps for reuse (the
- * only memory it holds across calls).  Bitmaps of 256 KiB and more are copied
- * before the host scan so the two overlap, and d_bitmap is then written
- * whatever the verdict.  h_bitmap must stay unchanged until the stream has
+ * The list is staged in pinned host memory the library keeps for reuse; the
+ * pinned staging, the device buffers and one copy stream per device are the
+ * only memory it holds across calls.  Bitmaps of 256 KiB and more are copied
+ * before the host scan so the two overlap (into d_bitmap on the fallback path,
+ * whatever the verdict).  h_bitmap must stay unchanged until the stream has
  * passed the call, as for any asynchronous copy. */
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                       size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream);

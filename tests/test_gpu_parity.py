@@ -7,6 +7,8 @@ edge shapes (S = 0/1, minimum block, ragged tiles, generic member counts).
 """
 from __future__ import annotations
 
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -387,6 +389,47 @@ def test_decode_tiling_policy(gpu, oracle, S, k, m, bs, kind, tiling):
             assert used in _valid_tilings(bm, k, m), used
     finally:
         gpu.set_decode_tiling(0)
+
+
+def test_decode_refuses_graph_capture(gpu, oracle):
+    """xec_decode scans h_bitmap on the host at call time, so a captured graph
+    would replay that call's losses whatever the bitmap held later: on a stream
+    being captured it returns XEC_DEVICE_ERROR with nothing queued (the capture
+    stays valid), as does xec_decode_per_stripe.  xec_decode_device is the
+    capturable form (tests/test_gpu_decode_device.py)."""
+    torch = _torch()
+    S, k, m, bs = 64, 16, 2, 4096
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    bm = _pattern("all", S, k, m, np.random.default_rng(3)).reshape(-1)
+    h_bm = torch.from_numpy(np.ascontiguousarray(bm)).pin_memory()
+    scratch = torch.empty(bm.size, dtype=torch.uint8, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=torch.cuda.Stream()):
+        cs = torch.cuda.current_stream()
+        assert gpu.decode(b.d, b.p, S, bs, k, m, h_bm, scratch, cs) == gpu.Status.DEVICE_ERROR
+        assert gpu.decode_per_stripe(b.d, b.p, S, bs, k, m, h_bm, scratch, None,
+                                     cs) == gpu.Status.DEVICE_ERROR
+    g.replay()  # an empty graph
+    torch.cuda.synchronize()
+    del g
+    erase_decode_check(gpu, b, ref_d, ref_p, bm)  # outside a capture: rebuilt
+
+
+def test_decode_scratch_upload_fallback():
+    """The fallback path of xec_decode's uploads (the caller's scratch, on the
+    stream) -- taken when no library buffer can be had, forced here with
+    XEC_SCRATCH_UPLOADS=1 in a child process: bitmap tiles, a device work list
+    longer than the kernel arguments hold, a list denser than the scratch, and
+    xec_decode_per_stripe's pieces, all checked against the oracle
+    (tests/scratch_uploads_check.py)."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, XEC_SCRATCH_UPLOADS="1")
+    p = subprocess.run([sys.executable, str(Path(__file__).parent / "scratch_uploads_check.py")],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0 and "scratch uploads ok" in p.stdout, p.stdout[-3000:] + p.stderr[-3000:]
 
 
 def test_golden_decode_fixtures_per_stripe(gpu, oracle, known_answers):
