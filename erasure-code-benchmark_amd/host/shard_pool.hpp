@@ -79,4 +79,29 @@ class ShardPool {
   bool stop_ = false;
 };
 
+// A one-shot barrier for the n calls of one ShardPool::run: arrive(ok) blocks
+// until all n have arrived and returns whether every one brought ok == true.
+// decode() checks every shard's bitmap slice first and launches only when all
+// are recoverable (all-or-nothing over the whole batch), inside one run().
+class Rendezvous {
+ public:
+  explicit Rendezvous(size_t n) : n_(n) {}
+  bool arrive(bool ok) {
+    std::unique_lock<std::mutex> lk(mu_);
+    all_ok_ = all_ok_ && ok;
+    if (++arrived_ == n_) {
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [this] { return arrived_ == n_; });
+    }
+    return all_ok_;
+  }
+
+ private:
+  size_t n_, arrived_ = 0;
+  bool all_ok_ = true;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+
 }  // namespace xec

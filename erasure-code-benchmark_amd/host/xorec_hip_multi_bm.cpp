@@ -138,37 +138,37 @@ int XorecBenchmarkHipMulti::encode() noexcept {
 }
 
 // All-or-nothing over the WHOLE batch, like the one-device plugin and the
-// reference's GPU decode (xorec_gpu_cmp.cu:75-81): every shard first checks its
-// slice of the host bitmap (xec_check_bitmap, is_recoverable per stripe,
-// xorec_utils.hpp:160-175), each on its own thread (m_pool); if any stripe of
-// any shard is unrecoverable the call returns DecodeFailure with nothing
-// launched on any device, so the bytes after a failed decode do not depend on
-// the device count.  Then every shard decodes its slice (xec_decode: host
-// scan, then the launch), again one thread each, so no device's launch waits
+// reference's GPU decode (xorec_gpu_cmp.cu:75-81): each shard's thread (m_pool)
+// first checks its slice of the host bitmap (xec_check_bitmap, is_recoverable
+// per stripe, xorec_utils.hpp:160-175), then all meet (Rendezvous); if any
+// stripe of any shard is unrecoverable no shard launches anything and the
+// call returns DecodeFailure, so the bytes after a failed decode do not depend
+// on the device count.  Otherwise every shard decodes its slice (xec_decode:
+// host scan, then the launch) on its own thread, so no device's launch waits
 // for another's scan; then every stream is waited for.
 int XorecBenchmarkHipMulti::decode() noexcept {
   const size_t n = m_shards.size();
   std::vector<int> st(n, XEC_DEVICE_ERROR);
+  Rendezvous all_recoverable(n);
+  bool launched = false;  // every shard reached xec_decode (written by shard 0)
   m_pool->run([&](size_t i) {
     const Shard& s = m_shards[i];
+    const uint8_t* bm = m_block_bitmap.get() + s.first * m_chunk_tot_blocks;
     int needs = 0;
-    st[i] = xec_check_bitmap(m_block_bitmap.get() + s.first * m_chunk_tot_blocks, s.count,
-                             m_chunk_data_blocks, m_chunk_parity_blocks, &needs);
-  });
-  for (int v : st)
-    if (v != XEC_SUCCESS) {
-      m_last_status = v;
-      return -1;
+    const int check = xec_check_bitmap(bm, s.count, m_chunk_data_blocks, m_chunk_parity_blocks,
+                                       &needs);
+    const bool go = all_recoverable.arrive(check == XEC_SUCCESS);
+    if (i == 0) launched = go;
+    if (!go) {
+      st[i] = check;  // this shard's own verdict (0 if only another shard failed)
+      return;
     }
-  m_pool->run([&](size_t i) {
-    const Shard& s = m_shards[i];
     const DeviceRestore restore;
     if (hipSetDevice(s.device) != hipSuccess) return;
     st[i] = xec_decode(s.data.get(), s.parity.get(), s.count, m_block_size, m_chunk_data_blocks,
-                       m_chunk_parity_blocks, m_block_bitmap.get() + s.first * m_chunk_tot_blocks,
-                       s.d_bitmap.get(), s.stream);
+                       m_chunk_parity_blocks, bm, s.d_bitmap.get(), s.stream);
   });
-  const bool ok = each([](const Shard&) { return true; });  // wait for every stream
+  const bool ok = !launched || each([](const Shard&) { return true; });  // wait for every stream
   int status = XEC_SUCCESS;
   for (int v : st)
     if (v != XEC_SUCCESS) {

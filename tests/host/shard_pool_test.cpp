@@ -1,7 +1,9 @@
 // ThreadSanitizer test of host/shard_pool.hpp (the multi-device plugin's
 // per-shard decode threads): every run() calls fn(i) exactly once per shard,
 // concurrently, and returns only after all of them; many back-to-back runs,
-// pool sizes 1..9, construction and destruction with idle workers.
+// pool sizes 1..9, construction and destruction with idle workers; and the
+// Rendezvous decode() uses inside one run: every call gets the AND of all
+// calls' flags, after all have arrived.
 #include <atomic>
 #include <cstdio>
 #include <vector>
@@ -25,6 +27,27 @@ int main() {
       for (size_t i = 0; i < n; ++i)
         if (hits[i] != round + 1) {
           std::printf("shard %zu ran %d times after %d rounds\n", i, hits[i], round + 1);
+          return 1;
+        }
+    }
+  }
+  for (size_t n = 1; n <= 9; ++n) {
+    xec::ShardPool pool(n);
+    for (int round = 0; round < 500; ++round) {
+      const size_t bad = static_cast<size_t>(round) % (n + 3);  // >= n: nobody fails
+      xec::Rendezvous rv(n);
+      std::vector<int> before(n, 0), verdict(n, -1);  // plain ints, as above
+      std::atomic<size_t> arrived{0};
+      pool.run([&](size_t i) {
+        before[i] = 1;
+        arrived.fetch_add(1);
+        const bool all = rv.arrive(i != bad);
+        if (arrived.load() != n) verdict[i] = 2;  // returned before everyone arrived
+        else verdict[i] = all ? 1 : 0;
+      });
+      for (size_t i = 0; i < n; ++i)
+        if (before[i] != 1 || verdict[i] != (bad >= n ? 1 : 0)) {
+          std::printf("rendezvous n=%zu round %d shard %zu: verdict %d\n", n, round, i, verdict[i]);
           return 1;
         }
     }
