@@ -1,0 +1,235 @@
+// read_probe.hip -- how fast this HBM reads under different address geometries
+// (a lab probe, NOT the product; standalone, no torch).
+//
+// Question: is the ~7.1 TB/s read-only rate measured on the encode's geometry
+// (16 streams 1 MiB apart, tools/lab/lab.py --ceiling, profiles/r01w) the
+// chip's read ceiling, or does the power-of-two member stride of the reference
+// batch layout (abstract_bm.cpp:4-18: block i of stripe c at c*k*bs + i*bs)
+// cost bandwidth that a different tile order could win back?
+//
+// Every kernel is the product's tile shape (csrc/xec_kernels.hip): one-wave
+// workgroups, each lane one 16-B granule of a 1 KiB chunk, NM loads in flight
+// per lane (all issued before the XOR), `nt` loads, the result stored only
+// under a never-true test so the loads stay live.  Only the addresses differ:
+//   tile t -> row r = t / tiles_per_row, chunk c = t % tiles_per_row,
+//   load q at  r*row_stride + c*1024 + lane*16 + q*member_stride.
+// Residency is capped as the product caps it (LDS reserved per workgroup).
+//
+// Build: make -C tools/lab read_probe   Run: tools/lab/read_probe [out.json]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Geo {
+  uint64_t row_stride, member_stride, tiles_per_row, total_tiles;
+  int reverse;  // walk tiles from the end (the product does)
+};
+
+template <int NM, bool NT>
+__global__ __launch_bounds__(64) void read_kernel(const uint8_t* __restrict__ base, Geo g,
+                                                  uint32_t magic, uint8_t* sink) {
+  const uint64_t t0 = blockIdx.x;
+  if (t0 >= g.total_tiles) return;
+  const uint64_t t = g.reverse ? g.total_tiles - 1 - t0 : t0;
+  const uint64_t r = t / g.tiles_per_row, c = t % g.tiles_per_row;
+  const uint8_t* p = base + r * g.row_stride + c * 1024 + threadIdx.x * 16;
+  u32x4 v[NM];
+#pragma unroll
+  for (int q = 0; q < NM; ++q) {
+    const u32x4* a = reinterpret_cast<const u32x4*>(p + (uint64_t)q * g.member_stride);
+    v[q] = NT ? __builtin_nontemporal_load(a) : *a;
+  }
+  u32x4 acc = v[0];
+#pragma unroll
+  for (int q = 1; q < NM; ++q) acc ^= v[q];
+  if (acc.x == magic && acc.y == magic && acc.z == magic && acc.w == magic)
+    *reinterpret_cast<u32x4*>(sink + threadIdx.x * 16) = acc;
+}
+
+// write-only: each workgroup writes `per_wg` contiguous KiB (one 1 KiB
+// wave-instruction per KiB), nt stores
+__global__ __launch_bounds__(64) void write_kernel(uint8_t* base, uint64_t tiles, int per_wg,
+                                                   uint32_t salt) {
+  const uint64_t t = blockIdx.x;
+  if (t >= tiles) return;
+  uint8_t* p = base + t * (uint64_t)per_wg * 1024 + threadIdx.x * 16;
+  for (int q = 0; q < per_wg; ++q) {
+    const u32x4 v = {(uint32_t)t ^ salt, (uint32_t)q, threadIdx.x, salt};
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p + q * 1024));
+  }
+}
+
+uint32_t lds_for_occupancy(int waves) {  // as csrc/xec_api.cpp, one-wave workgroups
+  if (waves <= 0 || waves >= 8) return 0;
+  uint32_t b = (160u * 1024u) / (uint32_t)(4 * waves);
+  b &= ~511u;
+  return b > 65536u ? 65536u : b;
+}
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,          \
+                   hipGetErrorString(e_));                                     \
+      std::exit(2);                                                            \
+    }                                                                          \
+  } while (0)
+
+struct Case {
+  std::string name;
+  int nm;
+  bool nt;
+  Geo g;
+};
+
+template <int NM, bool NT>
+void launch_read(const Case& cs, const uint8_t* buf, uint8_t* sink, uint32_t lds, hipStream_t s) {
+  read_kernel<NM, NT><<<dim3((uint32_t)cs.g.total_tiles), dim3(64), lds, s>>>(buf, cs.g, 0x9E3779B9u,
+                                                                              sink);
+}
+
+void launch(const Case& cs, const uint8_t* buf, uint8_t* sink, uint32_t lds, hipStream_t s) {
+  if (cs.nm == 16 && cs.nt) launch_read<16, true>(cs, buf, sink, lds, s);
+  else if (cs.nm == 16) launch_read<16, false>(cs, buf, sink, lds, s);
+  else if (cs.nm == 32 && cs.nt) launch_read<32, true>(cs, buf, sink, lds, s);
+  else if (cs.nm == 8 && cs.nt) launch_read<8, true>(cs, buf, sink, lds, s);
+  else std::exit(3);
+}
+
+double median(std::vector<float> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const char* out = argc > 1 ? argv[1] : nullptr;
+  const uint64_t KiB = 1024, MiB = KiB * KiB, GiB = MiB * KiB;
+  std::vector<Case> cases;
+  const uint64_t T16 = 4 * GiB / (16 * KiB);  // tiles of 16 x 1 KiB
+  // the encode at config 3: 256 stripes x 16 blocks of 1 MiB
+  cases.push_back({"cfg3_16x1MiB", 16, true, {16 * MiB, MiB, 1024, T16, 1}});
+  cases.push_back({"cfg3_16x1MiB_fwd", 16, true, {16 * MiB, MiB, 1024, T16, 0}});
+  cases.push_back({"cfg3_16x1MiB_default_policy", 16, false, {16 * MiB, MiB, 1024, T16, 1}});
+  // the same, member stride not a power of two
+  cases.push_back({"cfg3_members_1MiB+1KiB", 16, true, {16 * (MiB + KiB), MiB + KiB, 1024, T16, 1}});
+  cases.push_back({"cfg3_members_1MiB+4KiB", 16, true, {16 * (MiB + 4 * KiB), MiB + 4 * KiB, 1024, T16, 1}});
+  cases.push_back({"cfg3_members_1MiB+64KiB", 16, true, {16 * (MiB + 64 * KiB), MiB + 64 * KiB, 1024, T16, 1}});
+  // stripes (rows) not a power of two apart, members 1 MiB
+  cases.push_back({"cfg3_rows_16MiB+64KiB", 16, true, {16 * MiB + 64 * KiB, MiB, 1024, T16, 1}});
+  // one wave reads 16 KiB contiguous (16 consecutive 1 KiB pieces)
+  cases.push_back({"contig_16KiB_per_wave", 16, true, {16 * KiB, KiB, 1, T16, 1}});
+  cases.push_back({"contig_16KiB_per_wave_default_policy", 16, false, {16 * KiB, KiB, 1, T16, 1}});
+  // config 4's encode: 32 blocks of 4 KiB per stripe, 4 chunks per block
+  cases.push_back({"cfg4_32x4KiB", 32, true, {128 * KiB, 4 * KiB, 4, 4 * GiB / (32 * KiB), 1}});
+  // config 2's encode: 8 blocks of 64 KiB
+  cases.push_back({"cfg2_8x64KiB", 8, true, {512 * KiB, 64 * KiB, 64, 4 * GiB / (8 * KiB), 1}});
+
+  // Every byte a case reads must lie inside the buffers: the last tile's last
+  // member ends at (rows-1)*row_stride + tiles_per_row*1 KiB + (nm-1)*member_stride.
+  // The buffers are sized from that, checked again per case before it launches.
+  uint64_t need = 0;
+  auto end_of = [](const Case& cs) {
+    const uint64_t rows = (cs.g.total_tiles + cs.g.tiles_per_row - 1) / cs.g.tiles_per_row;
+    return (rows - 1) * cs.g.row_stride + cs.g.tiles_per_row * 1024 +
+           (uint64_t)(cs.nm - 1) * cs.g.member_stride;
+  };
+  for (const Case& cs : cases) need = std::max(need, end_of(cs));
+  need = std::max(need, GiB);  // the write streams cover exactly 1 GiB
+  need = (need + MiB - 1) / MiB * MiB;
+  std::printf("buffers: 2 x %llu MiB\n", (unsigned long long)(need / MiB));
+  uint8_t* bufs[2];
+  for (auto& b : bufs) {
+    CK(hipMalloc(&b, need));
+    CK(hipMemset(b, 0x5A, need));
+  }
+  uint8_t* sink;
+  CK(hipMalloc(&sink, 4096));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+
+  const int iters = 15;
+  const int occs[] = {0, 2, 4};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::string json = "{\n \"note\": \"read-only rates by address geometry, tools/lab/read_probe.hip\",\n \"results\": [\n";
+  bool first = true;
+  auto emit = [&](const std::string& name, int occ, double bytes, double ms) {
+    const double gbps = bytes / (ms * 1e-3) / 1e9;
+    std::printf("%-40s occ %d  %8.4f ms  %7.1f GB/s\n", name.c_str(), occ, ms, gbps);
+    std::fflush(stdout);
+    char line[256];
+    std::snprintf(line, sizeof line, "%s  {\"case\": \"%s\", \"waves_per_simd\": %d, \"ms_med\": %.4f, \"GBps_med\": %.1f}",
+                  first ? "" : ",\n", name.c_str(), occ, ms, gbps);
+    json += line;
+    first = false;
+  };
+  for (int round = 0; round < 2; ++round) {  // two interleaved passes
+    for (const Case& cs : cases) {
+      if (end_of(cs) > need || cs.g.total_tiles > 0x7fffffffu) {
+        std::fprintf(stderr, "case %s reaches %llu bytes of %llu: not launched\n", cs.name.c_str(),
+                     (unsigned long long)end_of(cs), (unsigned long long)need);
+        return 4;
+      }
+      for (int occ : occs) {
+        const uint32_t lds = lds_for_occupancy(occ);
+        launch(cs, bufs[0], sink, lds, s);  // warm-up
+        std::vector<float> ts;
+        for (int i = 0; i < iters; ++i) {
+          CK(hipEventRecord(e0, s));
+          launch(cs, bufs[(i + 1) % 2], sink, lds, s);
+          CK(hipEventRecord(e1, s));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ts.push_back(ms);
+        }
+        CK(hipGetLastError());
+        emit(cs.name + (round ? "#2" : ""), occ,
+             (double)cs.g.total_tiles * cs.nm * 1024.0, median(ts));
+      }
+    }
+    // write-only streams of 1 GiB, 1 / 4 KiB contiguous per workgroup
+    for (int per : {1, 4}) {
+      for (int occ : occs) {
+        const uint32_t lds = lds_for_occupancy(occ);
+        const uint64_t tiles = GiB / ((uint64_t)per * KiB);  // tiles * per KiB = 1 GiB <= need
+        std::vector<float> ts;
+        for (int i = 0; i < iters + 1; ++i) {
+          CK(hipEventRecord(e0, s));
+          write_kernel<<<dim3((uint32_t)tiles), dim3(64), lds, s>>>(bufs[i % 2], tiles, per, i);
+          CK(hipEventRecord(e1, s));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          if (i) ts.push_back(ms);
+        }
+        emit("write_1GiB_" + std::to_string(per) + "KiB_per_wg" + (round ? "#2" : ""), occ,
+             (double)GiB, median(ts));
+      }
+    }
+  }
+  json += "\n ]\n}\n";
+  if (out) {
+    FILE* f = std::fopen(out, "w");
+    if (f) {
+      std::fputs(json.c_str(), f);
+      std::fclose(f);
+    }
+  }
+  for (auto b : bufs) CK(hipFree(b));
+  CK(hipFree(sink));
+  return 0;
+}
