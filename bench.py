@@ -94,6 +94,9 @@ def parse():
                     help="skip the host-in/host-out leg (xec_pipeline, pinned host memory)")
     ap.add_argument("--host-stripes", type=int, default=0,
                     help="stripes per rank for the host-in/host-out leg (0 = 1 GiB of data)")
+    ap.add_argument("--rehearse-leg-delay", type=float, default=0.0,
+                    help="with --rehearse-cpu only: the scatter leg first sleeps this long, so "
+                         "a test can make the legs' watchdog fire deterministically")
     ap.add_argument("--rank-grace", type=float, default=60.0,
                     help="launcher: seconds to wait for the other ranks after one fails")
     return ap.parse_args()
@@ -353,13 +356,50 @@ def measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms, reps=
 HOST_CHUNK_STRIPES, HOST_STREAMS = 8, 3  # best measured pipeline shape
 
 
+def _cpulist(text):
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11} (sysfs cpulist format)."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def bind_numa_local(torch, dev, sysfs="/sys"):
+    """Keep this rank's host work and pinned buffers on its GPU's NUMA node.
+
+    On a two-socket 8-GPU node half the GPUs hang off each socket. A pinned
+    buffer on the far socket sends every byte of the host pipeline across the
+    socket link as well as over PCIe. Pinned pages are placed where the
+    allocating thread runs (default local policy), so the rank narrows its CPU
+    affinity to the node of its GPU's PCI function before it allocates them.
+    Returns {"numa_node": n, "cpus": c}, or a "skipped" reason when sysfs gives
+    no node or no allowed CPU lies on it. The affinity is left as it was then."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        node = int(Path(f"{sysfs}/bus/pci/devices/{bdf}/numa_node").read_text())
+        if node < 0:
+            return {"skipped": f"no NUMA node for {bdf}"}
+        local = _cpulist(Path(f"{sysfs}/devices/system/node/node{node}/cpulist").read_text())
+        mine = os.sched_getaffinity(0) & local
+        if not mine:
+            return {"skipped": f"no allowed CPU on node {node}"}
+        os.sched_setaffinity(0, mine)
+        return {"numa_node": node, "cpus": len(mine)}
+    except (OSError, ValueError, AttributeError) as e:
+        return {"skipped": repr(e)[:120]}
+
+
 def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3):
     """North star's end-to-end rate: each rank
     streams a batch that starts and ends in its own pinned host memory through
     its GPU with xec_pipeline (H2D -> kernel -> D2H, chunks over streams), all
     ranks at once between barriers.  Encode returns the parity to the host;
     decode rebuilds one lost data block per stripe in host memory.  Returns this
-    rank's (encode s, decode s, bit-exact, error); every rank makes the same
+    rank's (encode s, decode s, bit-exact, error, NUMA binding); every rank makes the same
     collective calls whatever fails locally.  PCIe-bound: reported beside, never
     as, the device-resident value."""
     import numpy as np
@@ -373,6 +413,9 @@ def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3
         return t.item() == 1.0
 
     err = None
+    # after the CPU baseline (which times the whole affinity mask), before any
+    # pinned buffer of this leg exists
+    numa = bind_numa_local(torch, torch.cuda.current_device())
     try:  # setup: pinned host batch, its parity and an erasure pattern
         h_d = torch.empty(S * k * bs, dtype=torch.uint8).pin_memory()
         h_p = torch.empty(S * m * bs, dtype=torch.uint8).pin_memory()
@@ -392,7 +435,7 @@ def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3
     except Exception as e:  # noqa: BLE001 - reported in the line
         err = repr(e)[:200]
     if not agree(err is None):
-        return 0.0, 0.0, False, err or "another rank failed its setup"
+        return 0.0, 0.0, False, err or "another rank failed its setup", numa
 
     rcs = []
 
@@ -418,7 +461,8 @@ def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3
     t_dec = timed(lambda: pl.decode(h_d, h_p, S, h_bm), before=erase)
     ok &= bool(torch.equal(h_d, ref_d)) and not any(rcs)
     pl.close()
-    return t_enc, t_dec, ok, (f"xec_pipeline status {sorted(set(rcs))}" if any(rcs) else None)
+    return (t_enc, t_dec, ok, (f"xec_pipeline status {sorted(set(rcs))}" if any(rcs) else None),
+            numa)
 
 
 def launch_ranks(n, argv, grace_s):
@@ -833,9 +877,10 @@ def run_rank(args):
         if host_leg:
             hs = args.host_stripes or max(1, (1 << 30) // (k * bs))
             with markers.region("bench:host_pipeline"):
-                t_enc, t_dec, ok_h, err = measure_host_pipeline(torch, dist, xec, k, m, bs, hs,
-                                                                start, coll_dev)
-            mine = torch.tensor([t_enc, t_dec, 1.0 if ok_h else 0.0], dtype=torch.float64,
+                t_enc, t_dec, ok_h, err, numa = measure_host_pipeline(
+                    torch, dist, xec, k, m, bs, hs, start, coll_dev)
+            mine = torch.tensor([t_enc, t_dec, 1.0 if ok_h else 0.0,
+                                 float(numa.get("numa_node", -1))], dtype=torch.float64,
                                 device=coll_dev)
             if use_dist:
                 hrows = [torch.zeros_like(mine) for _ in range(world)]
@@ -850,6 +895,8 @@ def run_rank(args):
                   "bit_exact": all(r[2] == 1.0 for r in hrows),
                   "per_rank_encode_GBps_data": [
                       round(hs * k * bs / r[0] / 1e9, 2) if r[0] else None for r in hrows],
+                  # each rank's pinned buffers on its GPU's NUMA node (-1: not bound)
+                  "per_rank_numa_node": [int(r[3]) for r in hrows],
                   "sample": f"{hs} stripes ({hs * k * bs >> 20} MiB data) per rank in pinned "
                             f"host memory, xec_pipeline {HOST_CHUNK_STRIPES}-stripe chunks x "
                             f"{HOST_STREAMS} streams, all ranks at once, best of 3 after a "
@@ -857,6 +904,8 @@ def run_rank(args):
                             "= survivors in, one rebuilt block per stripe out",
                   "note": "end-to-end, PCIe-bound (DESIGN.md §7); reported beside the "
                           "device-resident value, never as it"}
+            if "skipped" in numa:
+                hp["numa_bind_rank%d" % rank] = numa["skipped"]
             if err:
                 hp["error"] = err
                 print(f"rank {rank}: host_pipeline: {err}", file=sys.stderr)
@@ -865,6 +914,8 @@ def run_rank(args):
             try:
                 ops = DeviceOps(torch, xec, stream, k, m, bs)
                 ops.device, ops.sync = coll_dev, cuda.synchronize
+                if args.rehearse_cpu and args.rehearse_leg_delay > 0:
+                    time.sleep(args.rehearse_leg_delay)  # a stuck link, rehearsed
                 with markers.region("bench:scatter"):
                     sc = measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms)
             except Exception as e:  # noqa: BLE001 - report, keep the headline line

@@ -76,13 +76,15 @@ def test_launcher_propagates_rank_failure():
 
 @pytest.mark.parametrize("gpus", [1, 2])
 def test_hung_leg_is_visible_in_exit_status(gpus):
-    """The legs' watchdog (--scatter-timeout) fires while the scatter leg runs:
+    """The legs' watchdog (--scatter-timeout) fires while the scatter leg runs
+    (held up for longer than the watchdog by --rehearse-leg-delay; a bare short
+    watchdog raced a tiny leg that could finish first):
     rank 0 still prints exactly one line, carrying the leg's error, and the
     command -- the bench.py launcher at N=2, the lone rank at N=1 -- exits 3."""
     extra = ["--dist-world1"] if gpus == 1 else []
     p = _bench("--gpus", str(gpus), *extra, "--rehearse-cpu", "--dist-backend", "gloo",
                "--workload", "8,2,4096,5", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
-               "--scatter-timeout", "0.01", timeout=180)
+               "--scatter-timeout", "0.5", "--rehearse-leg-delay", "30", timeout=180)
     assert p.returncode == 3, (p.returncode, p.stderr[-3000:])
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
