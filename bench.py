@@ -797,6 +797,9 @@ def run_rank(args):
                        else "xec_decode",
                        "decode_tiling": args.decode_tiling or "automatic"},
             "roofline": dict(rl[dominant], dominant_by="avg launch time"),
+            # north star: the device-resident rate at every N also as a fraction of
+            # the HBM roofline of the N GPUs together (value / (N x 8 TB/s))
+            "value_frac_of_n_gpu_hbm_peak": round(value / (world * HBM_PEAK_GBPS), 4),
             "roofline_by_kernel": rl,
             "cpu_baseline": cpu,
             "encode_ms": round(enc_ms_max, 4),

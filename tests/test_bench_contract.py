@@ -47,10 +47,12 @@ def test_bench_json_line(workload, stripes):
     assert set(c["by_workload"]) == {"cfg2", "cfg3", "cfg4"}
     assert c["by_workload"][workload]["value"] == c["value"]
     assert out["value"] > 0
+    assert abs(out["value_frac_of_n_gpu_hbm_peak"] - out["value"] / 8000.0) < 1e-3
     assert out["dist"]["ranks_seen"] == 1 and len(out["per_rank"]) == 1
     hp = out["host_pipeline"]  # the north star's host-in / host-out leg
     assert hp["bit_exact"] is True and "error" not in hp, hp
     assert hp["encode_GBps_data"] > 0 and hp["decode_GBps_data"] > 0
+    assert len(hp["per_rank_numa_node"]) == 1  # -1 where sysfs names no node
 
 
 def test_bench_device_decode_api():

@@ -40,6 +40,8 @@ def test_launcher_plain_command(n):
     assert out["verified"] is True
     assert out["data"].startswith("CPU REHEARSAL")
     assert out["cpu_baseline"] is None  # the CPU leg is N=1 only
+    # the whole-job rate against the N GPUs' HBM together (north star)
+    assert abs(out["value_frac_of_n_gpu_hbm_peak"] - out["value"] / (n * 8000.0)) < 1e-3
     sc = out["scatter"]
     assert sc["bit_exact"] is True and sc["gathered_parity_bit_exact_vs_root_encode"] is True
     # max-over-ranks: the reported step time covers every rank's elapsed time
