@@ -356,39 +356,20 @@ def measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms, reps=
 HOST_CHUNK_STRIPES, HOST_STREAMS = 8, 3  # best measured pipeline shape
 
 
-def _cpulist(text):
-    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11} (sysfs cpulist format)."""
-    cpus = set()
-    for part in text.strip().split(","):
-        if not part:
-            continue
-        lo, _, hi = part.partition("-")
-        cpus.update(range(int(lo), int(hi or lo) + 1))
-    return cpus
-
-
-def bind_numa_local(torch, dev, sysfs="/sys"):
-    """Keep this rank's host work and pinned buffers on its GPU's NUMA node.
-
-    On a two-socket 8-GPU node half the GPUs hang off each socket. A pinned
-    buffer on the far socket sends every byte of the host pipeline across the
-    socket link as well as over PCIe. Pinned pages are placed where the
-    allocating thread runs (default local policy), so the rank narrows its CPU
-    affinity to the node of its GPU's PCI function before it allocates them.
-    Returns {"numa_node": n, "cpus": c}, or a "skipped" reason when sysfs gives
-    no node or no allowed CPU lies on it. The affinity is left as it was then."""
+def gpu_numa_node(torch, dev, sysfs="/sys"):
+    """The NUMA node of this rank's GPU (its PCI function in sysfs), for the
+    host leg's per-rank record: on a two-socket 8-GPU node half the GPUs hang
+    off each socket. HIP already places pinned host allocations on the node
+    nearest the current device (hipHostMalloc without hipHostMallocNumaUser),
+    so nothing is rebound here; the line shows where each rank's link ends.
+    Returns {"numa_node": n}, or a "skipped" reason."""
     try:
         pr = torch.cuda.get_device_properties(dev)
         bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
         node = int(Path(f"{sysfs}/bus/pci/devices/{bdf}/numa_node").read_text())
         if node < 0:
             return {"skipped": f"no NUMA node for {bdf}"}
-        local = _cpulist(Path(f"{sysfs}/devices/system/node/node{node}/cpulist").read_text())
-        mine = os.sched_getaffinity(0) & local
-        if not mine:
-            return {"skipped": f"no allowed CPU on node {node}"}
-        os.sched_setaffinity(0, mine)
-        return {"numa_node": node, "cpus": len(mine)}
+        return {"numa_node": node}
     except (OSError, ValueError, AttributeError) as e:
         return {"skipped": repr(e)[:120]}
 
@@ -399,7 +380,7 @@ def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3
     its GPU with xec_pipeline (H2D -> kernel -> D2H, chunks over streams), all
     ranks at once between barriers.  Encode returns the parity to the host;
     decode rebuilds one lost data block per stripe in host memory.  Returns this
-    rank's (encode s, decode s, bit-exact, error, NUMA binding); every rank makes the same
+    rank's (encode s, decode s, bit-exact, error, GPU NUMA node); every rank makes the same
     collective calls whatever fails locally.  PCIe-bound: reported beside, never
     as, the device-resident value."""
     import numpy as np
@@ -413,9 +394,7 @@ def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3
         return t.item() == 1.0
 
     err = None
-    # after the CPU baseline (which times the whole affinity mask), before any
-    # pinned buffer of this leg exists
-    numa = bind_numa_local(torch, torch.cuda.current_device())
+    numa = gpu_numa_node(torch, torch.cuda.current_device())
     try:  # setup: pinned host batch, its parity and an erasure pattern
         h_d = torch.empty(S * k * bs, dtype=torch.uint8).pin_memory()
         h_p = torch.empty(S * m * bs, dtype=torch.uint8).pin_memory()
@@ -898,7 +877,7 @@ def run_rank(args):
                   "bit_exact": all(r[2] == 1.0 for r in hrows),
                   "per_rank_encode_GBps_data": [
                       round(hs * k * bs / r[0] / 1e9, 2) if r[0] else None for r in hrows],
-                  # each rank's pinned buffers on its GPU's NUMA node (-1: not bound)
+                  # the NUMA node each rank's GPU hangs off (-1: sysfs names none)
                   "per_rank_numa_node": [int(r[3]) for r in hrows],
                   "sample": f"{hs} stripes ({hs * k * bs >> 20} MiB data) per rank in pinned "
                             f"host memory, xec_pipeline {HOST_CHUNK_STRIPES}-stripe chunks x "
@@ -908,7 +887,7 @@ def run_rank(args):
                   "note": "end-to-end, PCIe-bound (DESIGN.md §7); reported beside the "
                           "device-resident value, never as it"}
             if "skipped" in numa:
-                hp["numa_bind_rank%d" % rank] = numa["skipped"]
+                hp["numa_rank%d" % rank] = numa["skipped"]
             if err:
                 hp["error"] = err
                 print(f"rank {rank}: host_pipeline: {err}", file=sys.stderr)

@@ -76,36 +76,17 @@ def test_erasure_pattern_is_recoverable_and_exact():
             assert xo.np_is_recoverable(k, m, row) and xo.np_require_recovery(k, row)
 
 
-def test_cpulist_parses_sysfs_format():
-    assert bench._cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
-    assert bench._cpulist("5") == {5}
-    assert bench._cpulist("") == set()
-
-
-def test_bind_numa_local_narrows_affinity_to_the_gpu_node(tmp_path, monkeypatch):
-    """The host leg's ranks keep their pinned buffers on their GPU's NUMA node
-    (bench.bind_numa_local): a fake sysfs puts the GPU's PCI function on node 1."""
-    import os
+def test_gpu_numa_node_reads_the_pci_function(tmp_path):
+    """The host leg records the NUMA node of each rank's GPU (bench.gpu_numa_node)
+    from the PCI function in sysfs; a fake sysfs puts it on node 1."""
     from types import SimpleNamespace
 
-    allowed = sorted(os.sched_getaffinity(0))
-    node1 = allowed[len(allowed) // 2:] or allowed
     (tmp_path / "bus/pci/devices/0000:c1:00.0").mkdir(parents=True)
     (tmp_path / "bus/pci/devices/0000:c1:00.0/numa_node").write_text("1\n")
-    (tmp_path / "devices/system/node/node1").mkdir(parents=True)
-    (tmp_path / "devices/system/node/node1/cpulist").write_text(
-        ",".join(str(c) for c in node1) + "\n")
     props = SimpleNamespace(pci_domain_id=0, pci_bus_id=0xC1, pci_device_id=0)
     fake_torch = SimpleNamespace(cuda=SimpleNamespace(get_device_properties=lambda d: props))
-    got = {}
-    monkeypatch.setattr(bench.os, "sched_setaffinity", lambda pid, cpus: got.update(cpus=cpus))
-    out = bench.bind_numa_local(fake_torch, 0, sysfs=str(tmp_path))
-    assert out == {"numa_node": 1, "cpus": len(node1)}
-    assert got["cpus"] == set(node1)
-    # no node for the device (-1), or no sysfs entry at all: affinity untouched
-    got.clear()
+    assert bench.gpu_numa_node(fake_torch, 0, sysfs=str(tmp_path)) == {"numa_node": 1}
     (tmp_path / "bus/pci/devices/0000:c1:00.0/numa_node").write_text("-1\n")
-    assert "skipped" in bench.bind_numa_local(fake_torch, 0, sysfs=str(tmp_path))
-    props.pci_bus_id = 0x05
-    assert "skipped" in bench.bind_numa_local(fake_torch, 0, sysfs=str(tmp_path))
-    assert got == {}
+    assert "skipped" in bench.gpu_numa_node(fake_torch, 0, sysfs=str(tmp_path))
+    props.pci_bus_id = 0x05  # no such device
+    assert "skipped" in bench.gpu_numa_node(fake_torch, 0, sysfs=str(tmp_path))
