@@ -170,3 +170,76 @@ def test_random_shape_every_decode_path(gpu, oracle, case):
             assert np.array_equal(got, want), (path, S, k, m, bs)
     finally:
         gpu.set_decode_tiling(0)
+
+
+@pytest.mark.parametrize("S,k,m,bs", [(3, 1000, 1, 256), (2, 512, 2, 512), (3, 264, 8, 256),
+                                      (5, 1, 1, 256), (4, 2, 2, 768)])
+def test_wide_and_narrow_stripes_every_decode_path(gpu, oracle, S, k, m, bs):
+    """Stripes far wider than any BASELINE shape (k up to 1,000: the generic
+    member loop, past the work list's k <= 256) and the narrowest (k = m): the
+    reference puts no bound on k (xorec_utils.hpp:61-86 checks only k >= 1,
+    m >= 1, k % m == 0).  Every stripe loses one block per class; every decode
+    entry point rebuilds it bit-exactly, or refuses with InvalidSize where
+    its list cannot name the block (k > 256), touching nothing."""
+    import torch
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs, seed=5100 + k)
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(S):
+        oracle.select_lost_blocks(k, m, m, bm[c], 61 * k + c)
+        bm[c, k:] = 1  # data losses only: one per class
+        if not (bm[c, :k] == 0).any():
+            bm[c, c % k] = 0
+    h_bm = torch.from_numpy(bm.reshape(-1).copy()).pin_memory()
+    d_bm = h_bm.to("cuda")
+    ref_dt = torch.from_numpy(ref_d).to("cuda")
+    try:
+        for path in DECODE_PATHS:
+            b.d[: S * k * bs].copy_(ref_dt)
+            assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == 0
+            erased = b.data().copy()
+            st = _decode_via(gpu, path, b, h_bm, d_bm)
+            assert np.array_equal(b.parity(), ref_p), (path, "parity written")
+            if k > 256 and path in ("per_stripe", "device_list"):
+                assert st == gpu.Status.INVALID_SIZE and np.array_equal(b.data(), erased), path
+                continue
+            assert st == 0, (path, st)
+            assert np.array_equal(b.data(), ref_d), (path, S, k, m, bs)
+    finally:
+        gpu.set_decode_tiling(0)
+
+
+@pytest.mark.parametrize("extra", [0, 1])
+def test_stripe_count_at_the_work_list_limit(gpu, extra):
+    """S = 2^24 stripes is the most a work-list entry (stripe << 8 | block,
+    xec_internal.h) can name; one more and xec_decode must take the bitmap
+    tiles, xec_decode_per_stripe must refuse.  k=2+1, 256 B blocks (8 GiB of
+    data), sparse losses including the batch's last stripe.  Checked by the
+    round trip erase -> decode == pristine, parity untouched (the oracle would
+    take minutes at this size)."""
+    import torch
+    S, k, m, bs = (1 << 24) + extra, 2, 1, 256
+    s = torch.cuda.current_stream()
+    d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+    p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+    assert gpu.fill_splitmix64(d, S, k * bs, 777, s) == 0
+    assert gpu.encode(d, p, S, bs, k, m, s) == 0
+    pristine, p0 = d.clone(), p.clone()
+    bm = np.ones((S, k + m), np.uint8)
+    lost = np.r_[np.arange(0, S, 4099), S - 1]  # ~4,100 stripes: sparse -> list wanted
+    bm[lost, lost % k] = 0
+    h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
+    d_bm = h_bm.to("cuda")
+    del bm
+    assert gpu.erase(d, p, S, bs, k, m, d_bm, s) == 0
+    assert gpu.decode(d, p, S, bs, k, m, h_bm, torch.empty_like(d_bm), s) == 0
+    assert gpu.decode_tiling_used() == (3 if extra == 0 else 1)  # list / stripe tiles
+    assert torch.equal(d, pristine) and torch.equal(p, p0)
+    # the per-stripe entry point names blocks by list entry: refused past the limit
+    assert gpu.erase(d, p, S, bs, k, m, d_bm, s) == 0
+    st = gpu.decode_per_stripe(d, p, S, bs, k, m, h_bm, torch.empty_like(d_bm), None, s)
+    if extra:
+        assert st == gpu.Status.INVALID_SIZE
+        assert not torch.equal(d, pristine)  # refused before touching anything
+    else:
+        assert st == 0 and torch.equal(d, pristine)
+    assert torch.equal(p, p0)
