@@ -94,6 +94,14 @@ bool for_runs(size_t n, W&& want, F&& copy) {
 // in per-copy overhead than the bytes it saves.  With m = 1 both are the same.
 constexpr size_t kSelectiveCopyBytes = 64u << 10;
 
+// A chunk's outputs (parity, or rebuilt blocks) are queued after the next
+// chunk's inputs rather than right behind its own kernel, so the copy engine
+// has the next chunk's input queued before the host waits on anything
+// (tools/pageable_probe.py).  Measured: pinned encode +2.3 % (52.8 -> 54.0
+// GB/s at config 3, 8-stripe chunks x 3 streams, profiles/r03q), decode and
+// the pageable rates unchanged.
+constexpr bool kDeferOutputs = true;
+
 }  // namespace
 
 extern "C" {
@@ -142,23 +150,32 @@ xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_pari
   if (!p) return XEC_NOT_INITIALIZED;
   const DeviceGuard dg(p->device);
   if (!dg.ok) return XEC_DEVICE_ERROR;
-  const size_t k = p->k, m = p->m, bs = p->bs;
+  const size_t k = p->k, m = p->m, bs = p->bs, cs = p->chunk_stripes;
   const auto* src = static_cast<const uint8_t*>(h_data);
   auto* dst = static_cast<uint8_t*>(h_parity);
+  const size_t ns = p->slots.size();
+  // a chunk's parity copy-out is queued after the NEXT chunk's input (see
+  // kDeferOutputs); with one slot the next chunk would overwrite it first
+  const bool defer = kDeferOutputs && ns > 1;
+  auto out = [&](size_t chunk) {
+    const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
+    auto& s = p->slots[chunk % ns];
+    return hipMemcpyAsync(dst + c0 * m * bs, s.parity, n * m * bs, hipMemcpyDeviceToHost,
+                          s.stream) == hipSuccess;
+  };
   size_t chunk = 0;
-  for (size_t c0 = 0; c0 < S; c0 += p->chunk_stripes, ++chunk) {
-    auto& s = p->slots[chunk % p->slots.size()];
-    const size_t n = (S - c0) < p->chunk_stripes ? (S - c0) : p->chunk_stripes;
+  for (size_t c0 = 0; c0 < S; c0 += cs, ++chunk) {
+    auto& s = p->slots[chunk % ns];
+    const size_t n = (S - c0) < cs ? (S - c0) : cs;
     // stream order serialises reuse of this slot behind its previous chunk
     if (hipMemcpyAsync(s.data, src + c0 * k * bs, n * k * bs, hipMemcpyHostToDevice, s.stream) !=
         hipSuccess)
       return fail(p, XEC_DEVICE_ERROR);
     xec_status st = xec_encode(s.data, s.parity, n, bs, k, m, s.stream);
     if (st != XEC_SUCCESS) return fail(p, st);
-    if (hipMemcpyAsync(dst + c0 * m * bs, s.parity, n * m * bs, hipMemcpyDeviceToHost, s.stream) !=
-        hipSuccess)
-      return fail(p, XEC_DEVICE_ERROR);
+    if (defer ? (chunk > 0 && !out(chunk - 1)) : !out(chunk)) return fail(p, XEC_DEVICE_ERROR);
   }
+  if (defer && chunk > 0 && !out(chunk - 1)) return fail(p, XEC_DEVICE_ERROR);
   return sync_all(p);
 }
 
@@ -167,18 +184,38 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
   if (!p) return XEC_NOT_INITIALIZED;
   const DeviceGuard dg(p->device);
   if (!dg.ok) return XEC_DEVICE_ERROR;
-  const size_t k = p->k, m = p->m, bs = p->bs, row = k + m;
+  const size_t k = p->k, m = p->m, bs = p->bs, row = k + m, cs = p->chunk_stripes;
   int needs = 0;
   xec_status st = xec_check_bitmap(h_bitmap, S, k, m, &needs);
   if (st != XEC_SUCCESS || !needs) return st;  // all-or-nothing, as xec_decode
   auto* data = static_cast<uint8_t*>(h_data);
   const auto* par = static_cast<const uint8_t*>(h_parity);
   const bool selective = m > 1 && bs >= kSelectiveCopyBytes;
+  const size_t ns = p->slots.size();
+  const bool defer = kDeferOutputs && ns > 1;  // as in xec_pipeline_encode
   std::vector<uint8_t> class_lost(m);
-  size_t chunk = 0;
-  for (size_t c0 = 0; c0 < S; c0 += p->chunk_stripes, ++chunk) {
-    auto& s = p->slots[chunk % p->slots.size()];
-    const size_t n = (S - c0) < p->chunk_stripes ? (S - c0) : p->chunk_stripes;
+  // D2H of the rebuilt blocks of `chunk` (only those: a survivor's bytes are
+  // already in the caller's buffer)
+  auto out = [&](size_t chunk, size_t slot) {
+    const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
+    auto& s = p->slots[slot];
+    for (size_t c = c0; c < c0 + n; ++c) {
+      const uint8_t* bm = h_bitmap + c * row;
+      const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
+      if (!for_runs(k, [&](size_t i) { return bm[i] == 0; }, [&](size_t i, size_t j) {
+            return hipMemcpyAsync(data + base + i * bs, s.data + sbase + i * bs, (j - i) * bs,
+                                  hipMemcpyDeviceToHost, s.stream) == hipSuccess;
+          }))
+        return false;
+    }
+    return true;
+  };
+  // Slots go round the chunks that rebuild something (a chunk without a loss
+  // moves nothing), so consecutive rebuilding chunks never share a slot.
+  size_t chunk = 0, used = 0, pending = 0, pending_slot = 0;
+  bool have_pending = false;
+  for (size_t c0 = 0; c0 < S; c0 += cs, ++chunk) {
+    const size_t n = (S - c0) < cs ? (S - c0) : cs;
     bool any_lost = false;
     for (size_t c = c0; c < c0 + n && !any_lost; ++c)
       for (size_t i = 0; i < k; ++i)
@@ -187,6 +224,8 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
           break;
         }
     if (!any_lost) continue;  // nothing of this chunk crosses the link
+    const size_t slot = used++ % ns;
+    auto& s = p->slots[slot];
     // H2D: the surviving data blocks a rebuild reads (a lost block's content
     // is never read) and the parity; D2H: only the rebuilt blocks.  With
     // selective copies only the classes that lost a data block travel
@@ -214,16 +253,19 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
       return fail(p, XEC_DEVICE_ERROR);
     st = xec_decode(s.data, s.parity, n, bs, k, m, h_bitmap + c0 * row, s.bitmap, s.stream);
     if (st != XEC_SUCCESS) return fail(p, st);
-    for (size_t c = c0; c < c0 + n; ++c) {
-      const uint8_t* bm = h_bitmap + c * row;
-      const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
-      if (!for_runs(k, [&](size_t i) { return bm[i] == 0; }, [&](size_t i, size_t j) {
-            return hipMemcpyAsync(data + base + i * bs, s.data + sbase + i * bs, (j - i) * bs,
-                                  hipMemcpyDeviceToHost, s.stream) == hipSuccess;
-          }))
-        return fail(p, XEC_DEVICE_ERROR);
+    if (!defer) {
+      if (!out(chunk, slot)) return fail(p, XEC_DEVICE_ERROR);
+      continue;
     }
+    // the previous rebuilding chunk's outputs go behind this chunk's inputs
+    // (another slot); its own slot takes new inputs only ns >= 2 rebuilding
+    // chunks later, after these outputs are queued on its stream
+    if (have_pending && !out(pending, pending_slot)) return fail(p, XEC_DEVICE_ERROR);
+    pending = chunk;
+    pending_slot = slot;
+    have_pending = true;
   }
+  if (have_pending && !out(pending, pending_slot)) return fail(p, XEC_DEVICE_ERROR);
   return sync_all(p);
 }
 

@@ -57,3 +57,44 @@ def test_pipeline_rejects_bad_args(gpu):
         gpu.Pipeline(0, 4096, 4, 1)
     with pytest.raises(RuntimeError):
         gpu.Pipeline(8, 4096, 6, 4)
+
+
+@pytest.mark.parametrize("ns,lossy_chunks", [(3, [0, 3, 6]), (2, [0, 2, 4, 5]), (3, [1, 2, 7]),
+                                             (1, [0, 1, 4])])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_pipeline_decode_skipped_chunks_and_pageable(gpu, oracle, ns, lossy_chunks, pinned):
+    """A chunk's outputs are queued behind the next rebuilding chunk's inputs
+    (csrc/xec_pipeline.cpp kDeferOutputs), and chunks without a loss move
+    nothing: losses only in chunks that would share a slot if slots went round
+    every chunk (0, 3, 6 with 3 slots), so a slot taken over before its
+    rebuilt blocks were copied out would show.  Pageable host buffers (plain
+    numpy) as well as pinned ones: file and socket buffers are pageable."""
+    S, k, m, bs, chunk = 16, 8, 2, 8192, 2
+    ref_d, ref_p = oracle.batch(S, k, m, bs, seed_base=4400 + ns)
+
+    def host(a):
+        if not pinned:
+            return np.ascontiguousarray(a.reshape(-1)).copy()
+        t = _pinned(a.size)
+        t.numpy()[:] = a.reshape(-1)
+        return t
+
+    h_d, h_p = host(ref_d), host(ref_p)
+    view = (h_d if not pinned else h_d.numpy()).reshape(S, k, bs)
+    with gpu.Pipeline(chunk, bs, k, m, ns) as pl:
+        out_p = host(np.zeros_like(ref_p))
+        assert pl.encode(h_d, out_p, S) == gpu.Status.SUCCESS
+        assert np.array_equal(np.asarray(out_p if not pinned else out_p.numpy()).reshape(-1),
+                              ref_p.reshape(-1))
+        bm = np.ones((S, k + m), np.uint8)
+        for q in lossy_chunks:
+            for c in range(q * chunk, (q + 1) * chunk):
+                oracle.select_lost_blocks(k, m, 1 + c % m, bm[c], 91 * c + ns)
+                bm[c, k:] = 1  # data losses only
+                if not (bm[c, :k] == 0).any():
+                    bm[c, c % k] = 0
+        view[bm[:, :k] == 0] = 0
+        h_bm = host(bm)
+        assert pl.decode(h_d, h_p, S, h_bm) == gpu.Status.SUCCESS
+        got = np.asarray(h_d if not pinned else h_d.numpy()).reshape(-1)
+        assert np.array_equal(got, ref_d.reshape(-1))
