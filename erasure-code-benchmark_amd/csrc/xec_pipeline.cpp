@@ -11,11 +11,110 @@
 // overlap chunk i±1's copies and kernels.  PCIe, not HBM, bounds this path.
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "xec.h"
 #include "xec_kernels.h"
+
+namespace {
+
+// Results bound for PAGEABLE host memory (file or socket buffers).  A D2H
+// copy into pageable memory is staged by HIP and holds the calling thread
+// until the stream reaches it and the bytes are out: ~75 us per 1 MiB rebuilt
+// block at config 3, in series with the next chunk's (also host-synchronous)
+// input copies (rocprofv3 trace, profiles/r03v).  So such results go to a
+// pinned bounce buffer per slot (an asynchronous DMA) and this helper thread
+// moves them to their destinations once the copy's event has passed, while
+// the caller's thread already copies the next chunk in.
+class HostCopier {
+ public:
+  struct Piece {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t bytes;
+  };
+  HostCopier(int device, size_t nslots) : device_(device), busy_(nslots, 0) {
+    th_ = std::thread([this] { run(); });
+  }
+  ~HostCopier() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();  // the queue is drained first
+  }
+  // After `ev` has passed, copy `pieces` (out of slot's bounce buffer).
+  void push(size_t slot, hipEvent_t ev, std::vector<Piece>&& pieces) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++busy_[slot];
+      q_.push_back(Job{slot, ev, std::move(pieces)});
+    }
+    cv_.notify_all();
+  }
+  // The slot's bounce buffer (and its event) may be reused.
+  void wait_slot(size_t slot) {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return busy_[slot] == 0; });
+  }
+  // Every queued copy done; false if an event wait failed since the last drain.
+  bool drain() {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] {
+      for (size_t b : busy_)
+        if (b) return false;
+      return true;
+    });
+    const bool ok = !failed_;
+    failed_ = false;
+    return ok;
+  }
+
+ private:
+  struct Job {
+    size_t slot;
+    hipEvent_t ev;
+    std::vector<Piece> pieces;
+  };
+  void run() {
+    (void)hipSetDevice(device_);
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        j = std::move(q_.front());
+        q_.pop_front();
+      }
+      const bool ok = hipEventSynchronize(j.ev) == hipSuccess;
+      if (ok)
+        for (const Piece& pc : j.pieces) std::memcpy(pc.dst, pc.src, pc.bytes);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!ok) failed_ = true;
+        --busy_[j.slot];
+      }
+      done_cv_.notify_all();
+    }
+  }
+  int device_;
+  std::vector<size_t> busy_;  // queued jobs per slot
+  std::deque<Job> q_;
+  bool stop_ = false, failed_ = false;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::thread th_;
+};
+
+}  // namespace
 
 struct xec_pipeline {
   int device = 0;
@@ -25,27 +124,79 @@ struct xec_pipeline {
     uint8_t* data = nullptr;
     uint8_t* parity = nullptr;
     uint8_t* bitmap = nullptr;
+    // pageable destinations only: chunk_stripes*m*bs pinned bytes (a chunk's
+    // parity, or its rebuilt blocks -- at most m per stripe) and the event
+    // after the D2H copies into them
+    uint8_t* bounce = nullptr;
+    hipEvent_t out_done = nullptr;
   };
   std::vector<Slot> slots;
+  HostCopier* copier = nullptr;  // made on the first pageable destination
 };
 
 namespace {
 
 void destroy_slots(xec_pipeline* p) {
-  for (auto& s : p->slots) {
+  for (auto& s : p->slots)
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+  delete p->copier;  // drains its queue: nothing reads a bounce buffer after this
+  p->copier = nullptr;
+  for (auto& s : p->slots) {
     (void)hipFree(s.data);
     (void)hipFree(s.parity);
     (void)hipFree(s.bitmap);
+    (void)hipHostFree(s.bounce);
+    if (s.out_done) (void)hipEventDestroy(s.out_done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
   p->slots.clear();
 }
 
+// Whether the host buffer at q is pinned (page-locked and known to HIP).
+// Pageable memory is not registered and hipPointerGetAttributes fails on it;
+// the error is cleared so it cannot surface in a later hipGetLastError.
+bool host_pinned(const void* q) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Bounce buffers, their events and the helper thread, for results bound for
+// pageable memory; false if any of them cannot be had.
+bool ensure_bounce(xec_pipeline* p) {
+  const size_t bytes = p->chunk_stripes * p->m * p->bs;
+  for (auto& s : p->slots) {
+    if (s.bounce == nullptr &&
+        hipHostMalloc(reinterpret_cast<void**>(&s.bounce), bytes, hipHostMallocDefault) !=
+            hipSuccess) {
+      s.bounce = nullptr;
+      return false;
+    }
+    if (s.out_done == nullptr &&
+        hipEventCreateWithFlags(&s.out_done, hipEventDisableTiming) != hipSuccess) {
+      s.out_done = nullptr;
+      return false;
+    }
+  }
+  if (p->copier == nullptr) {
+    try {  // no exception crosses the C ABI (a thread may fail to start)
+      p->copier = new HostCopier(p->device, p->slots.size());
+    } catch (...) {
+      p->copier = nullptr;
+    }
+  }
+  return p->copier != nullptr;
+}
+
+// Every queued copy done, the helper's host copies included.
 xec_status sync_all(xec_pipeline* p) {
   xec_status st = XEC_SUCCESS;
   for (auto& s : p->slots)
     if (hipStreamSynchronize(s.stream) != hipSuccess) st = XEC_DEVICE_ERROR;
+  if (p->copier && !p->copier->drain()) st = XEC_DEVICE_ERROR;
   return st;
 }
 
@@ -96,10 +247,9 @@ constexpr size_t kSelectiveCopyBytes = 64u << 10;
 
 // A chunk's outputs (parity, or rebuilt blocks) are queued after the next
 // chunk's inputs rather than right behind its own kernel, so the copy engine
-// has the next chunk's input queued before the host waits on anything
-// (tools/pageable_probe.py).  Measured: pinned encode +2.3 % (52.8 -> 54.0
-// GB/s at config 3, 8-stripe chunks x 3 streams, profiles/r03q), decode and
-// the pageable rates unchanged.
+// has the next chunk's input queued before the host waits on anything.
+// Measured: pinned encode +2.3 % (52.8 -> 54.0 GB/s at config 3, 8-stripe
+// chunks x 3 streams, tools/pageable_probe.py, profiles/r03q).
 constexpr bool kDeferOutputs = true;
 
 }  // namespace
@@ -157,11 +307,23 @@ xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_pari
   // a chunk's parity copy-out is queued after the NEXT chunk's input (see
   // kDeferOutputs); with one slot the next chunk would overwrite it first
   const bool defer = kDeferOutputs && ns > 1;
+  // parity bound for pageable memory leaves through the bounce buffers
+  const bool bounce = S > 0 && !host_pinned(h_parity);
+  if (bounce && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
   auto out = [&](size_t chunk) {
     const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
-    auto& s = p->slots[chunk % ns];
-    return hipMemcpyAsync(dst + c0 * m * bs, s.parity, n * m * bs, hipMemcpyDeviceToHost,
-                          s.stream) == hipSuccess;
+    const size_t si = chunk % ns;
+    auto& s = p->slots[si];
+    if (!bounce)
+      return hipMemcpyAsync(dst + c0 * m * bs, s.parity, n * m * bs, hipMemcpyDeviceToHost,
+                            s.stream) == hipSuccess;
+    p->copier->wait_slot(si);
+    if (hipMemcpyAsync(s.bounce, s.parity, n * m * bs, hipMemcpyDeviceToHost, s.stream) !=
+            hipSuccess ||
+        hipEventRecord(s.out_done, s.stream) != hipSuccess)
+      return false;
+    p->copier->push(si, s.out_done, {{dst + c0 * m * bs, s.bounce, n * m * bs}});
+    return true;
   };
   size_t chunk = 0;
   for (size_t c0 = 0; c0 < S; c0 += cs, ++chunk) {
@@ -193,20 +355,42 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
   const bool selective = m > 1 && bs >= kSelectiveCopyBytes;
   const size_t ns = p->slots.size();
   const bool defer = kDeferOutputs && ns > 1;  // as in xec_pipeline_encode
+  // Pageable h_data: every copy to or from it holds this thread until done.
+  // The rebuilt blocks then leave through the bounce buffers, and a chunk's
+  // data comes in as ONE copy, lost blocks included (their content is never
+  // read), instead of one copy per run of survivors -- ~20 us of host time
+  // per call, against the 1/k more bytes (profiles/r03v).
+  const bool pageable = !host_pinned(h_data);
+  if (pageable && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
+  const bool whole_chunks = pageable && !selective;
   std::vector<uint8_t> class_lost(m);
   // D2H of the rebuilt blocks of `chunk` (only those: a survivor's bytes are
   // already in the caller's buffer)
   auto out = [&](size_t chunk, size_t slot) {
     const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
     auto& s = p->slots[slot];
+    std::vector<HostCopier::Piece> owed;
+    size_t off = 0;  // bounce offset: at most m rebuilt blocks per stripe
+    if (pageable) p->copier->wait_slot(slot);
     for (size_t c = c0; c < c0 + n; ++c) {
       const uint8_t* bm = h_bitmap + c * row;
       const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
       if (!for_runs(k, [&](size_t i) { return bm[i] == 0; }, [&](size_t i, size_t j) {
-            return hipMemcpyAsync(data + base + i * bs, s.data + sbase + i * bs, (j - i) * bs,
-                                  hipMemcpyDeviceToHost, s.stream) == hipSuccess;
+            const size_t bytes = (j - i) * bs;
+            uint8_t* to = data + base + i * bs;
+            if (pageable) {
+              owed.push_back({to, s.bounce + off, bytes});
+              to = s.bounce + off;
+              off += bytes;
+            }
+            return hipMemcpyAsync(to, s.data + sbase + i * bs, bytes, hipMemcpyDeviceToHost,
+                                  s.stream) == hipSuccess;
           }))
         return false;
+    }
+    if (pageable) {
+      if (hipEventRecord(s.out_done, s.stream) != hipSuccess) return false;
+      p->copier->push(slot, s.out_done, std::move(owed));
     }
     return true;
   };
@@ -230,7 +414,10 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
     // is never read) and the parity; D2H: only the rebuilt blocks.  With
     // selective copies only the classes that lost a data block travel
     // (xorec.cpp:79-108 reads nothing else).
-    for (size_t c = c0; c < c0 + n; ++c) {
+    if (whole_chunks && hipMemcpyAsync(s.data, data + c0 * k * bs, n * k * bs,
+                                       hipMemcpyHostToDevice, s.stream) != hipSuccess)
+      return fail(p, XEC_DEVICE_ERROR);
+    for (size_t c = c0; c < c0 + n && !whole_chunks; ++c) {
       const uint8_t* bm = h_bitmap + c * row;
       const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
       for (size_t j = 0; j < m; ++j) class_lost[j] = 0;

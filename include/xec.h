@@ -265,8 +265,9 @@ int xec_decode_tiling_used(void);
  * streams.  Host buffers may be pageable (file or socket buffers) or pinned
  * (hipHostMalloc / hipHostRegister); pinned ones run at the link's rate
  * (config 3: encode 54, decode 55 GB/s of data against 57 raw), pageable ones
- * at 52 / 43.  The calls return when the results are in host
- * memory.  Each call runs on the pipeline's device and leaves the caller's
+ * at 53 / 49.  Results bound for pageable memory go through
+ * pinned bounce buffers the pipeline owns, copied out by a helper thread of
+ * its own.  The calls return when the results are in host memory.  Each call runs on the pipeline's device and leaves the caller's
  * current device as it found it.  Same argument checks and status codes as
  * xec_encode / xec_decode. */
 typedef struct xec_pipeline xec_pipeline;

@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=HOST_CHUNK_STRIPES)
     ap.add_argument("--streams", type=int, default=HOST_STREAMS)
+    ap.add_argument("--kinds", default="pinned,pageable",
+                    help="comma list of: pinned, pageable, data_pageable_parity_pinned, "
+                         "data_pinned_parity_pageable")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -69,11 +72,20 @@ def main():
             ts.append(time.perf_counter() - t0)
         return min(ts[1:])
 
-    for kind in ("pinned", "pageable"):
+    # (data, parity) buffers: pinned or pageable each; the mixed pairs say
+    # which buffer a pageable slowdown comes from
+    kinds = {"pinned": (True, True), "pageable": (False, False),
+             "data_pageable_parity_pinned": (False, True),
+             "data_pinned_parity_pageable": (True, False)}
+    for kind, (pin_d, pin_p) in kinds.items():
+        if kind not in args.kinds.split(","):
+            continue
         h_d = torch.empty(nbytes, dtype=torch.uint8)
         h_p = torch.zeros(S * m * bs, dtype=torch.uint8)
-        if kind == "pinned":
-            h_d, h_p = h_d.pin_memory(), h_p.pin_memory()
+        if pin_d:
+            h_d = h_d.pin_memory()
+        if pin_p:
+            h_p = h_p.pin_memory()
         h_d.copy_(ref_d)
         r = {}
         r["h2d_GBps"] = round(nbytes / best(lambda: d_d.copy_(h_d, non_blocking=True)) / 1e9, 2)
