@@ -48,3 +48,19 @@ def gpu():
     assert st == xec.Status.SUCCESS, f"xec_init failed: {st!r}"
     torch.cuda.set_device(0)
     return xec
+
+
+def run_tsan(cmd, **kw):
+    """Run a ThreadSanitizer binary.  On kernels with high mmap randomisation
+    TSan can abort at start-up ("FATAL: ThreadSanitizer: unexpected memory
+    mapping", seen on one GPU box) before any test code runs; the run is then
+    repeated once with address-space randomisation off for that process
+    (`setarch -R`, which starts the binary before it touches any device)."""
+    import platform
+    import subprocess
+    p = subprocess.run(cmd, capture_output=True, text=True, **kw)
+    if p.returncode != 0 and "unexpected memory mapping" in p.stderr:
+        p = subprocess.run(["setarch", platform.machine(), "-R", *map(str, cmd)],
+                           capture_output=True, text=True, **kw)
+    return p
+

@@ -10,7 +10,7 @@ import subprocess
 
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, run_tsan
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
@@ -51,6 +51,6 @@ def test_shard_pool_tsan(tmp_path):
                     f"-I{ROOT / 'erasure-code-benchmark_amd' / 'host'}",
                     str(ROOT / "tests" / "host" / "shard_pool_test.cpp"), "-o", str(exe)],
                    check=True, capture_output=True)
-    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    p = run_tsan([str(exe)], timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert "shard_pool ok" in p.stdout

@@ -11,7 +11,7 @@ import subprocess
 
 import pytest
 
-from conftest import PKG_DIR, ROOT
+from conftest import PKG_DIR, ROOT, run_tsan
 
 BENCH = PKG_DIR / "bin" / "xec_bench"
 HEADER = ("name,err_msg,iterations,warmup_iterations,gpu_computation,gpu_blocks,threads_per_block,"
@@ -216,7 +216,7 @@ def test_overrides_per_thread_under_tsan():
     assert exe.exists(), "build with make -C tests/host"
     supp = ROOT / "tests" / "host" / "tsan.supp"  # HSA-internal new/delete only
     env = dict(os.environ, TSAN_OPTIONS=f"exitcode=23:halt_on_error=0:suppressions={supp}")
-    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    p = run_tsan([str(exe)], timeout=300, env=env)
     assert "ThreadSanitizer" not in p.stderr, p.stderr[-6000:]
     assert p.returncode == 0 and "tsan_overrides ok" in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
 

@@ -13,7 +13,8 @@ as erased (xec_decode_per_stripe: failing stripes only).
     python tools/fuzz_big.py [--cases 60] [--seed 1] [--out f.json]
     python tools/fuzz_big.py --pipeline ...   # the host-in/host-out pipeline instead
 
---pipeline: the batch lives in pinned host memory (32-512 MiB); xec_pipeline
+--pipeline: the batch lives in host memory (32-512 MiB; pinned, pageable, or
+pageable data with pinned parity, case by case); xec_pipeline
 encode must give the device encode's parity, and decode must restore the
 erased host batch (only classes that lost a data block travel at >= 64 KiB
 blocks, csrc/xec_pipeline.cpp), or leave it untouched when a stripe is
@@ -197,8 +198,15 @@ def pipeline_fuzz(args, np, torch, xec, s, rng):
         p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
         assert xec.fill_splitmix64(d, S, k * bs, 9000 + case, s) == 0
         assert xec.encode(d, p, S, bs, k, m, s) == 0
-        h_d = torch.empty(S * k * bs, dtype=torch.uint8).pin_memory()
-        h_p = torch.empty(S * m * bs, dtype=torch.uint8).pin_memory()
+        # host buffers pinned, pageable (file / socket buffers: the pipeline's
+        # bounce-buffer path), or pageable data with pinned parity, in turn
+        mem = ["pinned", "pageable", "mixed"][case % 3]
+        h_d = torch.empty(S * k * bs, dtype=torch.uint8)
+        h_p = torch.empty(S * m * bs, dtype=torch.uint8)
+        if mem == "pinned":
+            h_d = h_d.pin_memory()
+        if mem != "pageable":
+            h_p = h_p.pin_memory()
         h_d.copy_(d)
         ref_p = p.cpu()
         ref_d = h_d.clone()
@@ -223,7 +231,7 @@ def pipeline_fuzz(args, np, torch, xec, s, rng):
         else:
             dec_ok = st == 4 and bool(torch.equal(h_d, erased))
         row = {"case": case, "k": k, "m": m, "bs": bs, "S": S, "chunk": chunk, "streams": ns,
-               "MiB": round(S * k * bs / 2**20, 1), "pattern": kind,
+               "MiB": round(S * k * bs / 2**20, 1), "pattern": kind, "host_memory": mem,
                "recoverable": bool(rec.all()), "encode_ok": enc_ok, "decode_ok": dec_ok}
         log.append(row)
         bad = not (enc_ok and dec_ok)
