@@ -374,9 +374,10 @@ def gpu_numa_node(torch, dev, sysfs="/sys"):
         return {"skipped": repr(e)[:120]}
 
 
-def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3):
+def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3, pinned=True):
     """North star's end-to-end rate: each rank
-    streams a batch that starts and ends in its own pinned host memory through
+    streams a batch that starts and ends in its own host memory -- pinned, or
+    with pinned=False pageable like a file or socket buffer -- through
     its GPU with xec_pipeline (H2D -> kernel -> D2H, chunks over streams), all
     ranks at once between barriers.  Encode returns the parity to the host;
     decode rebuilds one lost data block per stripe in host memory.  Returns this
@@ -395,9 +396,11 @@ def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3
 
     err = None
     numa = gpu_numa_node(torch, torch.cuda.current_device())
-    try:  # setup: pinned host batch, its parity and an erasure pattern
-        h_d = torch.empty(S * k * bs, dtype=torch.uint8).pin_memory()
-        h_p = torch.empty(S * m * bs, dtype=torch.uint8).pin_memory()
+    try:  # setup: host batch, its parity and an erasure pattern
+        h_d = torch.empty(S * k * bs, dtype=torch.uint8)
+        h_p = torch.empty(S * m * bs, dtype=torch.uint8)
+        if pinned:
+            h_d, h_p = h_d.pin_memory(), h_p.pin_memory()
         d_d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
         d_p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
         st = torch.cuda.current_stream()
@@ -861,9 +864,13 @@ def run_rank(args):
             with markers.region("bench:host_pipeline"):
                 t_enc, t_dec, ok_h, err, numa = measure_host_pipeline(
                     torch, dist, xec, k, m, bs, hs, start, coll_dev)
+                # the same from pageable buffers (file / socket buffers)
+                pg_enc, pg_dec, ok_pg, err_pg, _ = measure_host_pipeline(
+                    torch, dist, xec, k, m, bs, hs, start, coll_dev, pinned=False)
+            err = err or err_pg
             mine = torch.tensor([t_enc, t_dec, 1.0 if ok_h else 0.0,
-                                 float(numa.get("numa_node", -1))], dtype=torch.float64,
-                                device=coll_dev)
+                                 float(numa.get("numa_node", -1)), pg_enc, pg_dec,
+                                 1.0 if ok_pg else 0.0], dtype=torch.float64, device=coll_dev)
             if use_dist:
                 hrows = [torch.zeros_like(mine) for _ in range(world)]
                 dist.all_gather(hrows, mine)
@@ -879,6 +886,13 @@ def run_rank(args):
                       round(hs * k * bs / r[0] / 1e9, 2) if r[0] else None for r in hrows],
                   # the NUMA node each rank's GPU hangs off (-1: sysfs names none)
                   "per_rank_numa_node": [int(r[3]) for r in hrows],
+                  "pageable": {
+                      "encode_GBps_data": round(data_all / max(r[4] for r in hrows) / 1e9, 2)
+                      if all(r[4] > 0 for r in hrows) else None,
+                      "decode_GBps_data": round(data_all / max(r[5] for r in hrows) / 1e9, 2)
+                      if all(r[5] > 0 for r in hrows) else None,
+                      "bit_exact": all(r[6] == 1.0 for r in hrows),
+                      "note": "the same batch in pageable host memory (file / socket buffers)"},
                   "sample": f"{hs} stripes ({hs * k * bs >> 20} MiB data) per rank in pinned "
                             f"host memory, xec_pipeline {HOST_CHUNK_STRIPES}-stripe chunks x "
                             f"{HOST_STREAMS} streams, all ranks at once, best of 3 after a "

@@ -53,6 +53,8 @@ def test_bench_json_line(workload, stripes):
     assert hp["bit_exact"] is True and "error" not in hp, hp
     assert hp["encode_GBps_data"] > 0 and hp["decode_GBps_data"] > 0
     assert len(hp["per_rank_numa_node"]) == 1  # -1 where sysfs names no node
+    pg = hp["pageable"]  # the same batch from pageable buffers (file / socket buffers)
+    assert pg["bit_exact"] is True and pg["encode_GBps_data"] > 0 and pg["decode_GBps_data"] > 0
 
 
 def test_bench_device_decode_api():
