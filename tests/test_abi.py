@@ -167,3 +167,42 @@ def test_set_occupancy_validation():
     assert xec.set_occupancy(9) == xec.Status.INVALID_SIZE
     for w in (1, 4, 8, 0):
         assert xec.set_occupancy(w) == xec.Status.SUCCESS
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_header_is_plain_c_and_links(tmp_path):
+    """The boundary is a C ABI: include/xec.h compiles as strict C99 (no C++,
+    no HIP headers needed: hipStream_t is an opaque pointer), and a C program
+    links against libxec_hip.so and runs its host-only entry points -- the
+    reference's argument checks (xorec_utils.hpp:61-86) and recoverability scan
+    (:144-175) -- without a GPU."""
+    src = tmp_path / "c_client.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include "xec.h"
+int main(void) {
+  static unsigned char bm[2 * 5];
+  int needs = -1;
+  void* data = (void*)(uintptr_t)64;  /* only the address is checked */
+  for (int i = 0; i < 10; ++i) bm[i] = 1;
+  if (xec_check_args(data, data, 4096, 4, 1) != XEC_SUCCESS) return 1;
+  if (xec_check_args(data, data, 100, 4, 1) != XEC_INVALID_SIZE) return 2;
+  if (xec_check_args((void*)(uintptr_t)65, data, 4096, 4, 1) != XEC_INVALID_ALIGNMENT) return 3;
+  if (xec_check_args(data, data, 4096, 6, 4) != XEC_INVALID_COUNTS) return 4;
+  bm[5 + 2] = 0;  /* stripe 1 lost data block 2 */
+  if (xec_check_bitmap(bm, 2, 4, 1, &needs) != XEC_SUCCESS || needs != 1) return 5;
+  bm[5 + 4] = 0;  /* ... and its class parity: unrecoverable */
+  if (xec_check_bitmap(bm, 2, 4, 1, &needs) != XEC_DECODE_FAILURE) return 6;
+  printf("%s %s\n", xec_status_string(XEC_DECODE_FAILURE), xec_build_info());
+  return 0;
+}
+''')
+    exe = tmp_path / "c_client"
+    lib_dir = xec.LIB_PATH.parent
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic",
+                    f"-I{ROOT / 'include'}", str(src), "-o", str(exe), f"-L{lib_dir}",
+                    "-lxec_hip", f"-Wl,-rpath,{lib_dir}"], check=True, capture_output=True)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, (p.returncode, p.stderr)
+    assert p.stdout.startswith("DecodeFailure xec-hip gfx950")
