@@ -414,8 +414,9 @@ constexpr size_t kCopyFirstBitmapBytes = 256u << 10;
 // against the better of them, profiles/r02n/tiling_uniform.json, r02o).
 constexpr uint64_t kListStripesNum = 3, kListStripesDen = 4;
 
-xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k, size_t m,
-                      const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream) {
+static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
+                              size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
+                              hipStream_t stream) {
   g_tiling_used = 0;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
@@ -529,11 +530,23 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
   return ok ? XEC_SUCCESS : XEC_DEVICE_ERROR;
 }
 
+// No exception crosses the C ABI: the host-side bookkeeping allocates (upload
+// buffers, pinned staging, their lists), and an allocation failure there is a
+// device error for the caller, not a std::terminate.
+xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k, size_t m,
+                      const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream) {
+  try {
+    return decode_impl(d_data, d_parity, S, bs, k, m, h_bitmap, d_bitmap, stream);
+  } catch (...) {
+    return XEC_DEVICE_ERROR;
+  }
+}
+
 int xec_decode_tiling_used(void) { return g_tiling_used; }
 
-xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, size_t bs,
-                                 size_t k, size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
-                                 uint8_t* h_codes, hipStream_t stream) {
+static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, size_t S, size_t bs,
+                                         size_t k, size_t m, const uint8_t* h_bitmap,
+                                         uint8_t* d_bitmap, uint8_t* h_codes, hipStream_t stream) {
   g_tiling_used = 0;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
@@ -591,6 +604,17 @@ xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, s
   }
   stage_release(sg, queued, stream);
   return ok ? verdict : XEC_DEVICE_ERROR;
+}
+
+xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, size_t bs,
+                                 size_t k, size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
+                                 uint8_t* h_codes, hipStream_t stream) {
+  try {  // as xec_decode
+    return decode_per_stripe_impl(d_data, d_parity, S, bs, k, m, h_bitmap, d_bitmap, h_codes,
+                                  stream);
+  } catch (...) {
+    return XEC_DEVICE_ERROR;
+  }
 }
 
 xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,

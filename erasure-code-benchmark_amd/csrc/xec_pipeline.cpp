@@ -256,7 +256,7 @@ constexpr bool kDeferOutputs = true;
 
 extern "C" {
 
-xec_status xec_pipeline_create(xec_pipeline** out, size_t chunk_stripes, size_t bs, size_t k,
+static xec_status create_impl(xec_pipeline** out, size_t chunk_stripes, size_t bs, size_t k,
                                size_t m, int nstreams) {
   if (!out) return XEC_INVALID_SIZE;
   *out = nullptr;
@@ -296,7 +296,7 @@ xec_status xec_pipeline_destroy(xec_pipeline* p) {
   return XEC_SUCCESS;
 }
 
-xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_parity, size_t S) {
+static xec_status encode_impl(xec_pipeline* p, const void* h_data, void* h_parity, size_t S) {
   if (!p) return XEC_NOT_INITIALIZED;
   const DeviceGuard dg(p->device);
   if (!dg.ok) return XEC_DEVICE_ERROR;
@@ -341,7 +341,7 @@ xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_pari
   return sync_all(p);
 }
 
-xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_parity, size_t S,
+static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parity, size_t S,
                                const uint8_t* h_bitmap) {
   if (!p) return XEC_NOT_INITIALIZED;
   const DeviceGuard dg(p->device);
@@ -454,6 +454,36 @@ xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_pari
   }
   if (have_pending && !out(pending, pending_slot)) return fail(p, XEC_DEVICE_ERROR);
   return sync_all(p);
+}
+
+// No exception crosses the C ABI: the host bookkeeping allocates (slots, run
+// lists, the helper thread), and a failure there is a device error for the
+// caller.  Whatever was queued is drained first, so nothing touches the
+// caller's buffers after the call returns.
+xec_status xec_pipeline_create(xec_pipeline** out, size_t chunk_stripes, size_t bs, size_t k,
+                               size_t m, int nstreams) {
+  try {
+    return create_impl(out, chunk_stripes, bs, k, m, nstreams);
+  } catch (...) {
+    return XEC_DEVICE_ERROR;
+  }
+}
+
+xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_parity, size_t S) {
+  try {
+    return encode_impl(p, h_data, h_parity, S);
+  } catch (...) {
+    return p ? fail(p, XEC_DEVICE_ERROR) : XEC_DEVICE_ERROR;
+  }
+}
+
+xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_parity, size_t S,
+                               const uint8_t* h_bitmap) {
+  try {
+    return decode_impl(p, h_data, h_parity, S, h_bitmap);
+  } catch (...) {
+    return p ? fail(p, XEC_DEVICE_ERROR) : XEC_DEVICE_ERROR;
+  }
 }
 
 }  // extern "C"
