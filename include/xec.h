@@ -267,7 +267,10 @@ int xec_decode_tiling_used(void);
  * (config 3: encode 54, decode 55 GB/s of data against 57 raw), pageable ones
  * at 53 / 49.  Results bound for pageable memory go through
  * pinned bounce buffers the pipeline owns, copied out by a helper thread of
- * its own.  The calls return when the results are in host memory.  Each call runs on the pipeline's device and leaves the caller's
+ * its own.  The calls return when the results are in host memory.  A
+ * pipeline serves one call at a time: threads that stream concurrently each
+ * create their own (the library's other entry points may be called from any
+ * thread).  Each call runs on the pipeline's device and leaves the caller's
  * current device as it found it.  Same argument checks and status codes as
  * xec_encode / xec_decode. */
 typedef struct xec_pipeline xec_pipeline;
