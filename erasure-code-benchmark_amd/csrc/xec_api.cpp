@@ -382,6 +382,9 @@ xec_status xec_init(int device_id) {
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return XEC_DEVICE_ERROR;
   if (device_id < 0 || device_id >= count) return XEC_DEVICE_ERROR;
   if (hipSetDevice(device_id) != hipSuccess) return XEC_DEVICE_ERROR;
+  // code objects onto the device now rather than at the first codec call
+  if (xec::preload_kernels() != hipSuccess || xec::preload_validate() != hipSuccess)
+    return XEC_DEVICE_ERROR;
   g_initialised.store(true, std::memory_order_release);
   return XEC_SUCCESS;
 }

@@ -96,5 +96,11 @@ hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t 
                           hipStream_t s);
 hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, uint32_t* d_bad,
                            hipStream_t s);
+// Load each kernel file's code object onto the current device.  HIP loads a
+// code object at the first launch of one of its kernels, ~10 ms on MI355X
+// (tools/latency/first_call.py, profiles/r03z); xec_init does it instead, so
+// the first codec call runs at the steady-state latency.
+hipError_t preload_kernels();
+hipError_t preload_validate();
 
 }  // namespace xec

@@ -610,4 +610,10 @@ hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_ba
   return hipGetLastError();
 }
 
+// Loads this file's code object onto the current device (see xec_kernels.h).
+hipError_t preload_kernels() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&fill_kernel));
+}
+
 }  // namespace xec

@@ -423,4 +423,10 @@ hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, ui
   return hipGetLastError();
 }
 
+// Loads this file's code object onto the current device (see xec_kernels.h).
+hipError_t preload_validate() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&serial_validate_kernel));
+}
+
 }  // namespace xec

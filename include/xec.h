@@ -49,7 +49,9 @@ typedef enum {
 
 /* Replaces xorec_gpu_init (xorec_gpu_cmp.cuh:14, .cu:7-27) and xorec_init
  * (xorec.hpp:39, xorec.cpp:16-22).  Selects `device_id` for the calling
- * thread and marks the library initialised.  Idempotent per device.  Unlike
+ * thread, loads the library's kernels onto it (~10 ms once per device and
+ * process, so the first codec call runs at steady-state latency) and marks
+ * the library initialised.  Idempotent per device.  Unlike
  * the reference it takes no k: recovery checks are sized per call, so the
  * COMPLETE_DATA_BITMAP first-call sizing bug (xorec.cpp:16-22) cannot occur. */
 xec_status xec_init(int device_id);
