@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--carved", type=int, default=2, help="sets carved from one allocation")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--alloc", default="torch",
+                    help="comma list of allocators for the --sets sets each: torch (caching "
+                         "allocator), hipmalloc, contiguous (hipExtMallocWithFlags "
+                         "hipDeviceMallocContiguous)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import numpy as np
@@ -45,9 +49,37 @@ def main():
     db, pb = S * k * bs, S * m * bs
     s = torch.cuda.current_stream()
     sets = {}
-    for i in range(args.sets):
-        sets[f"own{i}"] = (torch.empty(db, dtype=torch.uint8, device="cuda"),
-                           torch.empty(pb, dtype=torch.uint8, device="cuda"))
+    hip = None
+    keep = []
+
+    class Raw:  # a device buffer from the HIP runtime directly (torch's runtime)
+        def __init__(self, nbytes, flags):
+            import ctypes
+            nonlocal hip
+            if hip is None:
+                hip = ctypes.CDLL("libamdhip64.so")
+                hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+                hip.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p),
+                                                      ctypes.c_size_t, ctypes.c_uint]
+            ptr = ctypes.c_void_p()
+            rc = (hip.hipMalloc(ctypes.byref(ptr), nbytes) if flags is None else
+                  hip.hipExtMallocWithFlags(ctypes.byref(ptr), nbytes, flags))
+            assert rc == 0 and ptr.value, f"allocation failed ({rc})"
+            self.ptr = ptr.value
+            keep.append(self)
+
+        def data_ptr(self):
+            return self.ptr
+
+    for a in args.alloc.split(","):
+        for i in range(args.sets):
+            if a == "torch":
+                d = torch.empty(db, dtype=torch.uint8, device="cuda")
+                p = torch.empty(pb, dtype=torch.uint8, device="cuda")
+            else:
+                flags = None if a == "hipmalloc" else 0x4  # hipDeviceMallocContiguous
+                d, p = Raw(db, flags), Raw(pb, flags)
+            sets[f"{'own' if a == 'torch' else a}{i}"] = (d, p)
     if args.carved:
         big = torch.empty(args.carved * (db + pb), dtype=torch.uint8, device="cuda")
         for i in range(args.carved):
