@@ -811,6 +811,14 @@ def run_rank(args):
                     "stdev_ms": round(statistics.stdev(v), 4) if len(v) > 1 else 0.0,
                     "min_ms": round(min(v), 4), "max_ms": round(max(v), 4)}
                 for n, v in (("encode", enc_list), ("decode", dec_list))},
+            # the same launches by resident buffer set: where a set's pages sit in
+            # HBM moves its rate by a few % (DESIGN.md §3 *Placement*); step i
+            # encodes set i % NSETS and decodes set (i + NSETS - 1) % NSETS
+            "median_ms_by_set_rank0": {
+                n: [round(statistics.median(
+                    [t for i, t in enumerate(v) if (args.warmup + i + shift) % NSETS == q]), 4)
+                    if args.steps >= NSETS else None for q in range(NSETS)]
+                for n, v, shift in (("encode", enc_list, 0), ("decode", dec_list, NSETS - 1))},
         }
     else:
         out = None

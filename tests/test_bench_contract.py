@@ -48,6 +48,8 @@ def test_bench_json_line(workload, stripes):
     assert c["by_workload"][workload]["value"] == c["value"]
     assert out["value"] > 0
     assert abs(out["value_frac_of_n_gpu_hbm_peak"] - out["value"] / 8000.0) < 1e-3
+    by_set = out["median_ms_by_set_rank0"]  # placement is visible per resident set
+    assert all(len(by_set[n]) == 3 and all(t > 0 for t in by_set[n]) for n in ("encode", "decode"))
     assert out["dist"]["ranks_seen"] == 1 and len(out["per_rank"]) == 1
     hp = out["host_pipeline"]  # the north star's host-in / host-out leg
     assert hp["bit_exact"] is True and "error" not in hp, hp
