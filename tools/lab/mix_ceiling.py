@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--shapes", default=SHAPES)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--sets", type=int, default=3,
+                    help="resident buffer sets (rotated); each row also gives every "
+                         "variant's median per set (placement, DESIGN.md §3)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -78,7 +81,7 @@ def main():
         nm = k // m
         lds = lds_for(AUTO_OCC[nm])
         sets = []
-        for s in range(3):
+        for s in range(args.sets):
             d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
             p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
             assert xec.fill_splitmix64(d, S, k * bs, 1000 + s * 7919, stream) == 0
@@ -89,30 +92,33 @@ def main():
         items = torch.from_numpy(((cs.astype(np.uint32) << 8) | ids.astype(np.uint32))).cuda()
         n_items = int(items.numel())
         h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
-        scratch = [torch.empty(S * (k + m), dtype=torch.uint8, device="cuda") for _ in range(3)]
+        scratch = [torch.empty(S * (k + m), dtype=torch.uint8, device="cuda")
+                   for _ in range(args.sets)]
         b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
         b_read = n_items * nm * bs  # k/m - 1 survivors + the class parity
         b_write = n_items * bs
         assert b_read + b_write == b_dec
 
         def run(v, i):
-            d, p = sets[i % 3]
+            d, p = sets[i % args.sets]
             if v == "encode":
                 return xec.encode(d, p, S, bs, k, m, stream)
             if v in ("decode", "auto"):
-                return xec.decode(d, p, S, bs, k, m, h_bm, scratch[i % 3], stream)
+                return xec.decode(d, p, S, bs, k, m, h_bm, scratch[i % args.sets], stream)
             mode = {"read": 0, "write": 1, "lab": 2, "spread": 3}[v]
             return L.mix_launch(mode, d.data_ptr(), p.data_ptr(), items.data_ptr(), n_items,
                                 k, m, bs, lds, sp)
 
         variants = ["decode", "auto", "read", "write", "lab", "spread", "encode"]
         times = {v: [] for v in variants}
+        by_set = {v: [[] for _ in range(args.sets)] for v in variants}
         it = 0
         for _ in range(args.rounds):
             for v in variants:
                 assert xec.set_decode_tiling(3 if v == "decode" else 0) == 0
                 evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                        for _ in range(args.iters)]
+                first = it
                 for e0, e1 in evs:
                     e0.record(stream)
                     assert run(v, it) == 0, v
@@ -120,6 +126,8 @@ def main():
                     it += 1
                 torch.cuda.synchronize()
                 times[v] += [a.elapsed_time(b) for a, b in evs]
+                for j, (a, b) in enumerate(evs):
+                    by_set[v][(first + j) % args.sets].append(a.elapsed_time(b))
         assert xec.set_decode_tiling(0) == 0
         # the product decode, bit-exact on a fresh batch
         d, p = sets[0]
@@ -147,7 +155,9 @@ def main():
                "mix_ceiling_TBps": round(b_dec / ceiling_ms / 1e9, 3),
                "decode_over_ceiling": round(ceiling_ms / med["decode"], 4),
                "auto_over_ceiling": round(ceiling_ms / med["auto"], 4),
-               "decode_frac_8TBps": round(b_dec / med["decode"] / 1e9 / 8.0, 4)}
+               "decode_frac_8TBps": round(b_dec / med["decode"] / 1e9 / 8.0, 4),
+               "median_ms_by_set": {v: [round(statistics.median(t), 4) if t else None
+                                        for t in by_set[v]] for v in variants}}
         print(json.dumps(row), flush=True)
         rows.append(row)
         del sets, fresh, scratch, items
