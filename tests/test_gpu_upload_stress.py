@@ -103,3 +103,99 @@ def test_concurrent_decodes_share_upload_buffers(gpu):
     for t, seen in tilings.items():
         name = list(SHAPES)[t % len(SHAPES)]
         assert seen == {SHAPES[name][5]}, f"thread {t} ({name}) used tilings {seen}"
+
+
+def test_concurrent_per_stripe_decodes_and_pipelines(gpu):
+    """The other users of the shared host-side state, concurrently: threads
+    running xec_decode_per_stripe (pinned list staging + upload buffers, list
+    longer than the kernel arguments hold) beside threads each streaming its
+    own pipeline over pageable buffers (bounce buffers + helper thread), with
+    an unrecoverable stripe in every other per-stripe batch.  Round trips are
+    checked against the pristine bytes; per-stripe codes against the pattern."""
+    import torch
+
+    errors: list[str] = []
+
+    def per_stripe(t: int):
+        k, m, bs, S = 8, 2, 512, 3000
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+                p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+                assert gpu.fill_splitmix64(d, S, k * bs, 77000 + t, s) == 0
+                assert gpu.encode(d, p, S, bs, k, m, s) == 0
+                pristine, p0 = d.clone(), p.clone()
+                for it in range(8):
+                    bm = np.ones((S, k + m), np.uint8)
+                    c = np.arange(S)
+                    bm[c, (c + it + t) % k] = 0  # one data block per stripe: 3,000 entries
+                    bad = (it % 2 == 1)
+                    if bad:  # stripe 17 loses a data block and its class parity
+                        bm[17, :] = 1
+                        bm[17, 0] = 0
+                        bm[17, k] = 0
+                    h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
+                    d_bm = h_bm.to("cuda", non_blocking=True)
+                    codes = np.full(S, 9, np.uint8)
+                    assert gpu.erase(d, p, S, bs, k, m, d_bm, s) == 0
+                    st = gpu.decode_per_stripe(d, p, S, bs, k, m, h_bm, torch.empty_like(d_bm),
+                                               codes, s)
+                    s.synchronize()
+                    want = np.zeros(S, np.uint8)
+                    if bad:
+                        want[17] = 4
+                    if st != (4 if bad else 0) or not np.array_equal(codes, want):
+                        errors.append(f"per-stripe thread {t} it {it}: status {st}")
+                        return
+                    got = d.view(S, k * bs)
+                    ok_rows = torch.ones(S, dtype=torch.bool)
+                    if bad:
+                        ok_rows[17] = False
+                        # the failing stripe is left as erased (its class-0 parity
+                        # too): restore it for the next round
+                        d.view(S, k * bs)[17].copy_(pristine.view(S, k * bs)[17])
+                        p.copy_(p0)
+                    if not torch.equal(got[ok_rows], pristine.view(S, k * bs)[ok_rows]):
+                        errors.append(f"per-stripe thread {t} it {it}: bytes")
+                        return
+        except Exception as e:  # noqa: BLE001 - collected and asserted below
+            errors.append(f"per-stripe thread {t}: {e!r}")
+
+    def pipeline(t: int):
+        k, m, bs, S = 16, 1, 65536, 96
+        try:
+            torch.cuda.set_device(0)
+            d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
+            p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
+            assert gpu.fill_splitmix64(d, S, k * bs, 88000 + t, torch.cuda.current_stream()) == 0
+            assert gpu.encode(d, p, S, bs, k, m, torch.cuda.current_stream()) == 0
+            ref_d, ref_p = d.cpu().numpy(), p.cpu().numpy()
+            h_d, h_p = ref_d.copy(), np.zeros_like(ref_p)  # pageable
+            with gpu.Pipeline(4, bs, k, m, 3) as pl:
+                for it in range(4):
+                    h_p[:] = 0
+                    if pl.encode(h_d, h_p, S) != 0 or not np.array_equal(h_p, ref_p):
+                        errors.append(f"pipeline thread {t} it {it}: encode")
+                        return
+                    bm = np.ones((S, k + m), np.uint8)
+                    c = np.arange(S)
+                    sel = (c + it) % 3 == 0
+                    bm[c[sel], ((c + t) % k)[sel]] = 0
+                    h_d.reshape(S, k, bs)[bm[:, :k] == 0] = 0
+                    if pl.decode(h_d, h_p, S, bm.reshape(-1).copy()) != 0 or \
+                            not np.array_equal(h_d, ref_d):
+                        errors.append(f"pipeline thread {t} it {it}: decode")
+                        return
+        except Exception as e:  # noqa: BLE001 - collected and asserted below
+            errors.append(f"pipeline thread {t}: {e!r}")
+
+    threads = [threading.Thread(target=per_stripe, args=(t,)) for t in range(8)]
+    threads += [threading.Thread(target=pipeline, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads), "a worker did not finish"
+    assert not errors, errors
