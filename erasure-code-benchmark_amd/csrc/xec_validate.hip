@@ -234,15 +234,20 @@ __device__ uint32_t window_crc(uint32_t W, const Segment& sg, bool active, int s
   return cur;
 }
 
-// Chain over the head, bytes 8..kSeg-1 (every lane of the group, same addresses).
-__device__ __forceinline__ uint32_t head_crc(const uint8_t* blk, uint32_t crc) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(blk);
-  for (int i = 2; i < kSeg / 4; ++i) crc = word_chain(crc, w[i]);
-  return crc;
-}
+// Validation walks the whole block as segments 0.. of kSeg bytes.  Segment 0
+// holds the 8-byte header (checksum, size) and then the first payload bytes;
+// the chain starts at byte 8 from the size (utils.cpp:72-97).  Lane 0 takes
+// segment 0 with its header words read as zero: eight zero bytes only rotate
+// the state (rotl3 eight times is rotl 24, and adding 0 never carries), so a
+// chain started at rotl(bs, 8) reaches exactly bs at byte 8 and continues as
+// the reference's.  The header then costs one lane's segment, not a serial
+// chain of 120 bytes that every lane of the wave walks first (round 3: that
+// chain was as many instructions per wave as the whole split window at 4 KiB
+// blocks).
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return (x << 8) | (x >> 24); }
 
 // Requires bs % kSeg == 0, bs >= 2 kSeg, 16-B aligned blocks; G >= the
-// segments per block past the head, or 64.  Windows of G*kSeg bytes.
+// segments per block, or 64.  Windows of G*kSeg bytes.
 template <int G>
 __global__ __launch_bounds__(64) void wave_validate_kernel(const uint8_t* data, uint64_t nblocks,
                                                            uint64_t bs, uint32_t* bad) {
@@ -260,13 +265,17 @@ __global__ __launch_bounds__(64) void wave_validate_kernel(const uint8_t* data, 
       for (int t = 0; t < kSeg / 16; ++t) sg.g[t] = src[t];
     };
     Segment cur;
-    load(cur, kSeg);
-    uint32_t W = head_crc(blk, (uint32_t)bs);
+    load(cur, 0);
+    if (sub == 0) {  // the header reads as zero (above)
+      cur.g[0][0] = 0u;
+      cur.g[0][1] = 0u;
+    }
+    uint32_t W = rotl8((uint32_t)bs);
     if constexpr (G < 64) {  // G covers the block: one window
-      W = window_crc<G>(W, cur, valid && kSeg + (uint64_t)sub * kSeg < bs, sub);
+      W = window_crc<G>(W, cur, valid && (uint64_t)sub * kSeg < bs, sub);
     } else {  // the next window's segment is in flight while this one is reduced
       Segment nxt;
-      for (uint64_t base = kSeg; base < bs; base += kWin) {
+      for (uint64_t base = 0; base < bs; base += kWin) {
         if (base + kWin < bs) load(nxt, base + kWin);
         W = window_crc<G>(W, cur, base + (uint64_t)sub * kSeg < bs, sub);
         cur = nxt;
@@ -348,11 +357,12 @@ __global__ __launch_bounds__(64) void wave_pattern_kernel(uint8_t* data, uint64_
   }
 }
 
-// Lanes per block: segments past the head, rounded up to a power of two, at
-// most a wave.  0 = the block does not tile into segments (lane kernels).
-int group_lanes(uint64_t bs) {
+// Lanes per block, rounded up to a power of two, at most a wave: the pattern
+// kernel's segments past the head (head = true), or all of the validate
+// kernel's segments.  0 = the block does not tile into segments (lane kernels).
+int group_lanes(uint64_t bs, bool head = true) {
   if (bs < 2 * kSeg || bs % kSeg != 0) return 0;
-  const uint64_t segs = bs / kSeg - 1;
+  const uint64_t segs = bs / kSeg - (head ? 1 : 0);
   int g = 1;
   while (g < 64 && (uint64_t)g < segs) g <<= 1;
   return g;
@@ -412,7 +422,7 @@ hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, ui
   if (hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
   if (nblocks == 0) return hipSuccess;
   const uint8_t* d = static_cast<const uint8_t*>(d_data);
-  const int g = group_lanes(bs);
+  const int g = group_lanes(bs, false);
   // Grouped lanes read each segment with 16-B loads a lane walks in order;
   // the lane kernel's strided walk loses even with 2 M blocks (profiles/r02e).
   if (g && g_validate_mode != 1)

@@ -36,24 +36,33 @@ def horner(seg: bytes) -> int:
     return s
 
 
-def split_crc(blk: bytes, bs: int, stats: dict) -> int:
-    """Mirror of wave_crc() in xec_validate.hip (head serial, then windows)."""
-    W = chain(bs & M32, blk[8:SEG])            # bytes 8..255, every lane redundantly
-    for base in range(SEG, bs, LANES * SEG):
-        segs = [blk[base + j * SEG: base + (j + 1) * SEG] if base + j * SEG < bs else b""
-                for j in range(LANES)]
+def rotl8(x: int) -> int:
+    return ((x << 8) | (x >> 24)) & M32
+
+
+def split_crc(blk: bytes, bs: int, stats: dict, lanes: int = LANES) -> int:
+    """Mirror of wave_validate_kernel in xec_validate.hip: the block as
+    segments of SEG bytes from byte 0, `lanes` per window.  Segment 0's first 8
+    bytes (the header) read as zero and the chain starts at rotl(bs, 8): eight
+    zero bytes rotate that to bs exactly at byte 8, where the reference chain
+    starts (utils.cpp:72-97)."""
+    W = rotl8(bs & M32)
+    data = bytes(8) + blk[8:bs]
+    for base in range(0, bs, lanes * SEG):
+        segs = [data[base + j * SEG: base + (j + 1) * SEG] if base + j * SEG < bs else b""
+                for j in range(lanes)]
         S = [horner(s) for s in segs]
         starts, acc = [], 0
-        for j in range(LANES):
+        for j in range(lanes):
             starts.append(W if j == 0 else oc_add(W, acc))
             acc = oc_add(acc, S[j])
-        ends = [chain(starts[j], segs[j]) for j in range(LANES)]
-        if all(ends[j] == starts[j + 1] for j in range(LANES - 1)):
+        ends = [chain(starts[j], segs[j]) for j in range(lanes)]
+        if all(ends[j] == starts[j + 1] for j in range(lanes - 1)):
             W = ends[-1]
         else:
             stats["fallback"] = stats.get("fallback", 0) + 1
             cur = W
-            for j in range(LANES):
+            for j in range(lanes):
                 cur = chain(cur, segs[j])
             W = cur
     return W

@@ -33,7 +33,7 @@ def test_split_falls_back_on_a_carry_and_stays_exact(lane):
     bs = 65536
     rng = np.random.default_rng(lane)
     blk = bytearray(rng.integers(0, 256, bs, dtype=np.uint8).tobytes())
-    pos = SEG + lane * SEG + 100          # inside `lane`'s segment of window 0
+    pos = lane * SEG + 100                # inside `lane`'s segment of window 0
     steer_to_carry(blk, bs, pos)
     stats: dict = {}
     assert split_crc(bytes(blk), bs, stats) == serial_crc(bytes(blk), bs)
@@ -65,3 +65,21 @@ def test_horner_is_chain_mod_ones_complement():
             carries = (carries * 8 + (t >> 32)) % M32
             y = t & M32
         assert y % M32 == (x + horner(seg) - carries) % M32
+
+
+@pytest.mark.parametrize("bs,lanes", [(4096, 32), (256, 2), (384, 4), (65536, 64)])
+def test_header_folded_into_segment_zero(bs, lanes):
+    """The kernel reads the 8 header bytes as zero and starts at rotl(bs, 8):
+    exact for any header content, and through a carry steered into the
+    header's own segment (bytes 8..127), at every group width it uses."""
+    rng = np.random.default_rng(bs + lanes)
+    for header in (bytes(8), bytes([0xFF]) * 8, rng.integers(0, 256, 8, dtype=np.uint8).tobytes()):
+        blk = bytearray(rng.integers(0, 256, bs, dtype=np.uint8).tobytes())
+        blk[:8] = header
+        assert split_crc(bytes(blk), bs, {}, lanes) == serial_crc(bytes(blk), bs)
+    blk = bytearray(rng.integers(0, 256, bs, dtype=np.uint8).tobytes())
+    steer_to_carry(blk, bs, 60)           # a carry inside segment 0, after the header
+    stats: dict = {}
+    assert split_crc(bytes(blk), bs, stats, lanes) == serial_crc(bytes(blk), bs)
+    assert stats.get("fallback", 0) >= 1
+

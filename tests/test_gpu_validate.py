@@ -77,17 +77,18 @@ def test_pattern_survives_encode_erase_decode(gpu):
 
 def _host_blocks_with_carries(nblocks, bs, seed):
     """Random blocks whose checksum chain carries out of 32 bits inside the
-    wave kernel's segments (lanes 0, 5, 62 of window 0, lane 30 of the last),
-    headers set to the reference checksum: the wave split must take its
-    lane-after-lane fallback there and still agree (tests/crc_model.py)."""
+    wave kernel's segments (lanes 0 -- the segment that also holds the header
+    --, 5 and 62 of window 0, lane 30 of the last), headers set to the
+    reference checksum: the wave split must take its lane-after-lane fallback
+    there and still agree (tests/crc_model.py)."""
     from crc_model import SEG, serial_crc, steer_to_carry
     rng = np.random.default_rng(seed)
     out = np.empty((nblocks, bs), np.uint8)
     for b in range(nblocks):
         blk = bytearray(rng.integers(0, 256, bs, dtype=np.uint8).tobytes())
         lanes = [0, 5, 62]
-        last = SEG + ((bs - SEG - 1) // (64 * SEG)) * 64 * SEG
-        pos = [SEG + ln * SEG + 40 + 7 * b for ln in lanes] + [last + 30 * SEG + 9]
+        last = ((bs - 1) // (64 * SEG)) * 64 * SEG
+        pos = [ln * SEG + 40 + 7 * b for ln in lanes] + [last + 30 * SEG + 9]
         for q in sorted(p for p in pos if p + 1 < bs):
             steer_to_carry(blk, bs, q)
         crc = serial_crc(bytes(blk), bs)
