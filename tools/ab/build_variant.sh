@@ -12,7 +12,7 @@ tmp=$(mktemp -d)
 trap 'rm -rf "$tmp"' EXIT
 cp -r "$root/erasure-code-benchmark_amd" "$root/include" "$tmp/"
 rm -rf "$tmp/erasure-code-benchmark_amd/build" "$tmp/erasure-code-benchmark_amd/xec/"*.so
-python3 "$patch" "$tmp/erasure-code-benchmark_amd/csrc/xec_kernels.hip"
+python3 "$patch" "$tmp/erasure-code-benchmark_amd/csrc/${XEC_PATCH_FILE:-xec_kernels.hip}"
 make -C "$tmp/erasure-code-benchmark_amd" -j8 xec/libxec_hip.so >/dev/null
 cp "$tmp/erasure-code-benchmark_amd/xec/libxec_hip.so" "$root/tools/ab/libxec_$name.so"
 echo "$root/tools/ab/libxec_$name.so"
