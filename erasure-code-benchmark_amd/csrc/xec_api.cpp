@@ -235,6 +235,22 @@ bool side_uploads() {
   return !off;
 }
 
+// Uploads go off the caller's stream only while that stream is busy: then a
+// copy queued on it would wait for the kernel before it (the bubble above).
+// On an idle stream -- a synchronous caller such as the reference's
+// BM_generic loop, which synchronises after every call -- the copy on the
+// stream starts at once, and the side path's cross-stream event would only
+// add latency: 8 MiB (40/32) with 8 lost ran at 2,284 instead of 3,669
+// Gbit/s per call, 128 MiB with 2-8 lost 21-27 % slower (tools/ab/
+// refrows_ab.sh, profiles/r03zk).  A NotReady answer is cleared so that no
+// later hipGetLastError reads it as a launch failure.
+bool stream_busy(hipStream_t stream) {
+  const hipError_t q = hipStreamQuery(stream);
+  if (q == hipSuccess) return false;
+  (void)hipGetLastError();
+  return true;
+}
+
 bool capturing(hipStream_t stream) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(stream, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
@@ -429,10 +445,18 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   // replay this call's losses whatever the bitmap holds then.  Refused before
   // anything is queued; xec_decode_device is the capturable form.
   if (capturing(stream)) return XEC_DEVICE_ERROR;
+  const size_t bitmap_bytes = S * (k + m);
+  const bool copy_first = bitmap_bytes >= kCopyFirstBitmapBytes;
+  // Small bitmaps are scanned first: a batch that needs no recovery (or
+  // cannot be recovered) returns before any device query or copy.
+  XecScan scan;
+  if (!copy_first) {
+    st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
+    if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) return st;
+  }
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
-  const bool side = side_uploads();
-  const size_t bitmap_bytes = S * (k + m);
+  const bool side = side_uploads() && stream_busy(stream);
   // The bitmap goes to the device (a library buffer, or the caller's scratch
   // on `stream`); for large bitmaps before the scan, so the two overlap.
   Upload bmu;
@@ -443,13 +467,13 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
     return hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice, stream) ==
            hipSuccess;
   };
-  const bool copy_first = bitmap_bytes >= kCopyFirstBitmapBytes;
-  if (copy_first && !upload_bitmap()) return XEC_DEVICE_ERROR;
-  XecScan scan;
-  st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
-  if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) {
-    upload_end(bmu, stream, false);  // only the bitmap copy was queued, if anything
-    return st;                       // failure, or nothing to rebuild
+  if (copy_first) {
+    if (!upload_bitmap()) return XEC_DEVICE_ERROR;
+    st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
+    if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) {
+      upload_end(bmu, stream, false);  // only the bitmap copy was queued
+      return st;                       // failure, or nothing to rebuild
+    }
   }
   // Which tiling: list tiles when the losses are sparse (or forced); for a
   // list short enough to travel in the kernel arguments also wherever stripe
@@ -585,7 +609,7 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
   (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, n, &n, &failures);
   g_tiling_used = XEC_TILING_LIST;
   Upload lu;
-  if (side_uploads() && upload_begin(items, n * 4, dev, lu)) {
+  if (side_uploads() && stream_busy(stream) && upload_begin(items, n * 4, dev, lu)) {
     stage_release(sg, true, lu.cs);
     const bool ok = upload_join(lu, stream) &&
                     xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,

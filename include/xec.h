@@ -78,10 +78,12 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * of lost data blocks the host scan found (4 bytes each; the list drives one
  * tile per lost block and 1 KiB chunk, xec_set_decode_tiling) -- is copied to
  * device buffers the library keeps, on a copy stream of its own that does not
- * wait for `stream`'s earlier work; `stream` waits only for that copy before
- * the decode kernel.  Up to 1,024 list entries travel in the kernel arguments
- * instead, and then nothing is copied.  d_bitmap is scratch for the call,
- * written on `stream` only when no library buffer can be had.  Not
+ * wait for `stream`'s earlier work, when `stream` is busy at the call; `stream`
+ * waits only for that copy before the decode kernel.  When `stream` is idle
+ * (a synchronous caller) the copy goes into d_bitmap on `stream` itself, which
+ * then starts at once without a cross-stream hand-off.  Up to 1,024 list
+ * entries travel in the kernel arguments instead, and then nothing is copied.
+ * d_bitmap is scratch for the call.  Not
  * capturable: the host scan reads h_bitmap at call time, so a graph would
  * replay this call's losses -- on a stream being captured the call returns
  * XEC_DEVICE_ERROR with nothing queued (xec_decode_device is the capturable
