@@ -44,6 +44,14 @@ def main():
     ap.add_argument("--lost", type=int, default=1, help="lost data blocks per stripe (1..m)")
     ap.add_argument("--tiling", type=int, default=0,
                     help="xec_set_decode_tiling for every lib (0 = automatic)")
+    ap.add_argument("--pattern", default="rotating", choices=["rotating", "same", "random"],
+                    help="which data block a stripe loses (--lost 1 only): bench.py's "
+                         "(7c) mod k, block 0 everywhere (one failed device), or seeded random")
+    ap.add_argument("--launch", default="",
+                    help="unroll,block_threads for xec_set_launch on every lib (default: none)")
+    ap.add_argument("--variants", default="",
+                    help="semicolon list of unroll,block_threads,occupancy launch variants to "
+                         "cross with --libs in the same process (0,0,0 = the library's default)")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the identical-results check (diagnostic builds that store elsewhere)")
     ap.add_argument("--out", default="")
@@ -58,6 +66,9 @@ def main():
     assert xec.init(0) == 0
     loaded = {n: load(n) for n in args.libs.split(",")}
     for L in loaded.values():
+        if args.launch:
+            u, t = (int(x) for x in args.launch.split(","))
+            assert L.xec_set_launch(u, 0, 0, t) == 0
         if hasattr(L, "xec_set_decode_tiling"):  # round-1 builds predate the call
             assert L.xec_set_decode_tiling(args.tiling) == 0
         else:
@@ -65,6 +76,11 @@ def main():
     occs = [int(x) for x in args.occ.split(",")] if args.occ else [None]
     libs = {}
     for n, L in loaded.items():
+        if args.variants:
+            for v in args.variants.split(";"):
+                u, t, o = (int(x) for x in v.split(","))
+                libs[f"{n}@u{u}t{t}o{o}"] = (L, (u, t, o))
+            continue
         for o in occs:
             libs[n if o is None else f"{n}@o{o}"] = (L, o)
     if args.workload in WORKLOADS:
@@ -80,6 +96,12 @@ def main():
         assert xec.fill_splitmix64(d, S, k * bs, 1896 + 7919 * i, s) == 0
         sets.append((d, p))
     bm = erasure_pattern(np, S, k, m, args.lost)
+    if args.pattern != "rotating":
+        assert args.lost == 1, "--pattern needs --lost 1"
+        bm[:] = 1
+        lost = (np.zeros(S, dtype=np.int64) if args.pattern == "same"
+                else np.random.default_rng(1896).integers(0, k, S))
+        bm[np.arange(S), lost] = 0
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
     scratch = h_bm.to("cuda")
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
@@ -88,7 +110,10 @@ def main():
     # every build must produce the same parity and the same rebuilt data
     ref = None
     def use(L, o):
-        if o is not None:
+        if isinstance(o, tuple):
+            assert L.xec_set_launch(o[0], 0, 0, o[1]) == 0
+            assert L.xec_set_occupancy(o[2]) == 0
+        elif o is not None:
             assert L.xec_set_occupancy(o) == 0
         return L
 
@@ -125,7 +150,7 @@ def main():
                 sets[i % 2][0].data_ptr(), sets[i % 2][1].data_ptr(), S, bs, k, m,
                 h_bm.data_ptr(), scratch.data_ptr(), sh))
     out = {"workload": args.workload, "k": k, "m": m, "bs": bs, "S": S, "lost": args.lost,
-           "libs": {}}
+           "pattern": args.pattern, "launch": args.launch, "libs": {}}
     for n, r in res.items():
         e, d = statistics.median(r["enc"]), statistics.median(r["dec"])
         out["libs"][n] = {"enc_ms_med": round(e, 4), "enc_GBps": round(b_enc / e / 1e6, 1),

@@ -32,7 +32,22 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct Geo {
   uint64_t row_stride, member_stride, tiles_per_row, total_tiles;
   int reverse;  // walk tiles from the end (the product does)
+  uint64_t alt_offset = 0;  // odd rows start this much further in (alternating classes)
+  // row order: 0 as laid out; p > 0 interleaves p groups of rows/p rows
+  // (consecutive tiles' rows are rows/p apart); -1 bit-reverses the row index
+  int perm = 0;
 };
+
+__device__ __forceinline__ uint64_t row_of(uint64_t r, const Geo& g) {
+  const uint64_t rows = (g.total_tiles + g.tiles_per_row - 1) / g.tiles_per_row;
+  if (g.perm > 0) return (r % g.perm) * (rows / g.perm) + r / g.perm;
+  if (g.perm < 0) {
+    uint64_t bits = 0;
+    while ((1ull << bits) < rows) ++bits;
+    return __brevll(r) >> (64 - bits);
+  }
+  return r;
+}
 
 template <int NM, bool NT>
 __global__ __launch_bounds__(64) void read_kernel(const uint8_t* __restrict__ base, Geo g,
@@ -40,8 +55,8 @@ __global__ __launch_bounds__(64) void read_kernel(const uint8_t* __restrict__ ba
   const uint64_t t0 = blockIdx.x;
   if (t0 >= g.total_tiles) return;
   const uint64_t t = g.reverse ? g.total_tiles - 1 - t0 : t0;
-  const uint64_t r = t / g.tiles_per_row, c = t % g.tiles_per_row;
-  const uint8_t* p = base + r * g.row_stride + c * 1024 + threadIdx.x * 16;
+  const uint64_t r = row_of(t / g.tiles_per_row, g), c = t % g.tiles_per_row;
+  const uint8_t* p = base + r * g.row_stride + (r & 1) * g.alt_offset + c * 1024 + threadIdx.x * 16;
   u32x4 v[NM];
 #pragma unroll
   for (int q = 0; q < NM; ++q) {
@@ -135,6 +150,20 @@ int main(int argc, char** argv) {
   cases.push_back({"cfg4_32x4KiB", 32, true, {128 * KiB, 4 * KiB, 4, 4 * GiB / (32 * KiB), 1}});
   // config 2's encode: 8 blocks of 64 KiB
   cases.push_back({"cfg2_8x64KiB", 8, true, {512 * KiB, 64 * KiB, 64, 4 * GiB / (8 * KiB), 1}});
+  // the 16+2 x 1 MiB single-erasure decode's data reads: 8 blocks 2 MiB apart
+  // in 16 MiB stripes, the class alternating from stripe to stripe (as the
+  // bench's erasure pattern makes it), against the same class every stripe
+  // and against 8 contiguous 1 MiB blocks
+  const uint64_t T8 = 4 * GiB / (8 * KiB);
+  cases.push_back({"d16p2_8x2MiB_alternating", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, MiB}});
+  cases.push_back({"d16p2_8x2MiB_same_class", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, 0}});
+  cases.push_back({"contig_8x1MiB", 8, true, {8 * MiB, MiB, 1024, T8, 1, 0}});
+  // the same-class reads in other row orders (which stripes are in flight together)
+  cases.push_back({"d16p2_same_class_rows_by2", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, 0, 2}});
+  cases.push_back({"d16p2_same_class_rows_by4", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, 0, 4}});
+  cases.push_back({"d16p2_same_class_rows_by16", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, 0, 16}});
+  cases.push_back({"d16p2_same_class_rows_bitrev", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, 0, -1}});
+  cases.push_back({"d16p2_alternating_rows_by4", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, MiB, 4}});
 
   // Every byte a case reads must lie inside the buffers: the last tile's last
   // member ends at (rows-1)*row_stride + tiles_per_row*1 KiB + (nm-1)*member_stride.
@@ -142,7 +171,7 @@ int main(int argc, char** argv) {
   uint64_t need = 0;
   auto end_of = [](const Case& cs) {
     const uint64_t rows = (cs.g.total_tiles + cs.g.tiles_per_row - 1) / cs.g.tiles_per_row;
-    return (rows - 1) * cs.g.row_stride + cs.g.tiles_per_row * 1024 +
+    return (rows - 1) * cs.g.row_stride + cs.g.alt_offset + cs.g.tiles_per_row * 1024 +
            (uint64_t)(cs.nm - 1) * cs.g.member_stride;
   };
   for (const Case& cs : cases) need = std::max(need, end_of(cs));
