@@ -246,6 +246,9 @@ def test_encode_is_linear(gpu):
     (21, 24, 8, 1024, "select"),    # reference select_lost_blocks, 1..m per stripe
     (9, 10, 5, 768, "all"),         # generic member count (k/m = 2, m = 5)
     (7, 15, 5, 512, "all"),         # generic member count 3
+    (16, 16, 2, 1 << 20, "device"),  # one failed device: the same data block in every stripe
+    (2048, 4, 1, 256, "device"),    # the same, past the kernel-argument list
+    (40, 32, 8, 4352, "devices"),   # two failed devices, in two classes
 ])
 def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
     """xec_set_decode_tiling: stripe tiles, class tiles, work-list tiles and the
@@ -270,6 +273,11 @@ def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
             if c % 5 == 0:
                 for j in range(m):
                     bm[c, j + m * int(rng.integers(k // m))] = 0
+        elif pattern == "device":
+            bm[c, k // 3] = 0
+        elif pattern == "devices":
+            bm[c, 1] = 0
+            bm[c, 2 * m] = 0  # class 0, while block 1 is in class 1
         elif pattern == "parity":
             lost_par = int(rng.integers(m))
             bm[c, k + lost_par] = 0
