@@ -441,18 +441,23 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
-  // The host scan reads h_bitmap now: a graph captured from this call would
-  // replay this call's losses whatever the bitmap holds then.  Refused before
-  // anything is queued; xec_decode_device is the capturable form.
-  if (capturing(stream)) return XEC_DEVICE_ERROR;
   const size_t bitmap_bytes = S * (k + m);
-  const bool copy_first = bitmap_bytes >= kCopyFirstBitmapBytes;
+  // The host scan reads h_bitmap now: a graph captured from this call would
+  // replay this call's losses whatever the bitmap holds then.  So a call with
+  // work to queue is refused on a capturing stream, before anything is
+  // queued; xec_decode_device is the capturable form.  A batch that needs no
+  // recovery, or cannot be recovered, returns its verdict from the scan
+  // alone, before any device call -- the reference's order
+  // (xorec_gpu_cmp.cu:75-81) -- so it never pays the capture query.
+  const bool cap = bitmap_bytes >= kCopyFirstBitmapBytes && capturing(stream);
+  const bool copy_first = bitmap_bytes >= kCopyFirstBitmapBytes && !cap;
   // Small bitmaps are scanned first: a batch that needs no recovery (or
   // cannot be recovered) returns before any device query or copy.
   XecScan scan;
   if (!copy_first) {
     st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
     if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) return st;
+    if (cap || capturing(stream)) return XEC_DEVICE_ERROR;
   }
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
@@ -580,12 +585,12 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
   if (st != XEC_SUCCESS) return st;
   if (S == 0) return XEC_SUCCESS;
   if (k > kWorkItemMaxK || S > kWorkItemMaxStripes) return XEC_INVALID_SIZE;
-  if (capturing(stream)) return XEC_DEVICE_ERROR;  // host scan now: see xec_decode
   uint64_t n = 0, failures = 0;
   st = xec_scan_stripes(h_bitmap, S, k, m, h_codes, nullptr, 0, &n, &failures);
   if (st != XEC_SUCCESS) return st;
   const xec_status verdict = failures ? XEC_DECODE_FAILURE : XEC_SUCCESS;
   if (n == 0) return verdict;
+  if (capturing(stream)) return XEC_DEVICE_ERROR;  // work to queue: see xec_decode
   const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   if (n <= xec::kArgItems) {

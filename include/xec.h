@@ -85,9 +85,12 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * entries travel in the kernel arguments instead, and then nothing is copied.
  * d_bitmap is scratch for the call.  Not
  * capturable: the host scan reads h_bitmap at call time, so a graph would
- * replay this call's losses -- on a stream being captured the call returns
- * XEC_DEVICE_ERROR with nothing queued (xec_decode_device is the capturable
- * form).
+ * replay this call's losses -- on a stream being captured a call with blocks
+ * to rebuild returns XEC_DEVICE_ERROR with nothing queued (xec_decode_device
+ * is the capturable form).  A batch that needs no recovery, or cannot be
+ * recovered, returns XEC_SUCCESS / XEC_DECODE_FAILURE from the host scan
+ * before any device call, capturing or not, as the reference decides before
+ * its first CUDA call (xorec_gpu_cmp.cu:75-81).
  * Lost parity is not regenerated.  Parity is READ-ONLY here, as in the CPU
  * decode (xorec.cpp:62-111) -- deliberately unlike the reference GPU decode,
  * which folds all data into parity (xorec_gpu_cmp.cu:94-102).  The content of

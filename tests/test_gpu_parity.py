@@ -424,6 +424,51 @@ def test_decode_refuses_graph_capture(gpu, oracle):
     erase_decode_check(gpu, b, ref_d, ref_p, bm)  # outside a capture: rebuilt
 
 
+def test_decode_verdicts_from_the_scan_under_capture(gpu, oracle):
+    """A batch with nothing to rebuild, or that cannot be rebuilt, gets its
+    verdict from the host scan before any device call -- the reference's order
+    (xorec_gpu_cmp.cu:75-81) -- also on a capturing stream; a batch with work
+    is refused there, small bitmap or one past the copy-before-scan size
+    (256 KiB), with nothing queued."""
+    torch = _torch()
+    S, k, m, bs = 64, 16, 2, 4096
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    none = np.ones(S * (k + m), np.uint8)
+    bad = none.reshape(S, k + m).copy()
+    bad[5, 0] = bad[5, 2] = 0  # two losses in class 0: unrecoverable
+    work = _pattern("all", S, k, m, np.random.default_rng(4)).reshape(-1)
+    # 32,768 stripes x 10 blocks = 320 KiB of bitmap: the copy-first size
+    Sb, kb, mb, bsb = 32768, 8, 2, 256
+    big = Batch(gpu, Sb, kb, mb, bsb)
+    assert gpu.encode(big.d, big.p, Sb, bsb, kb, mb, big.stream) == 0
+    big_none = np.ones(Sb * (kb + mb), np.uint8)
+    big_work = big_none.reshape(Sb, kb + mb).copy()
+    big_work[:, 3] = 0
+    pin = {n: torch.from_numpy(np.ascontiguousarray(x.reshape(-1))).pin_memory()
+           for n, x in (("none", none), ("bad", bad), ("work", work),
+                        ("big_none", big_none), ("big_work", big_work))}
+    scratch = torch.empty(Sb * (kb + mb), dtype=torch.uint8, device="cuda")
+    before = (b.data().copy(), big.data().copy())
+    St = gpu.Status
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=torch.cuda.Stream()):
+        cs = torch.cuda.current_stream()
+        assert gpu.decode(b.d, b.p, S, bs, k, m, pin["none"], scratch, cs) == St.SUCCESS
+        assert gpu.decode(b.d, b.p, S, bs, k, m, pin["bad"], scratch, cs) == St.DECODE_FAILURE
+        assert gpu.decode(b.d, b.p, S, bs, k, m, pin["work"], scratch, cs) == St.DEVICE_ERROR
+        assert gpu.decode(big.d, big.p, Sb, bsb, kb, mb, pin["big_none"], scratch,
+                          cs) == St.SUCCESS
+        assert gpu.decode(big.d, big.p, Sb, bsb, kb, mb, pin["big_work"], scratch,
+                          cs) == St.DEVICE_ERROR
+        assert gpu.decode_per_stripe(b.d, b.p, S, bs, k, m, pin["none"], scratch, None,
+                                     cs) == St.SUCCESS
+    g.replay()  # an empty graph: nothing was queued
+    torch.cuda.synchronize()
+    del g
+    assert np.array_equal(b.data(), before[0]) and np.array_equal(big.data(), before[1])
+
+
 def test_decode_scratch_upload_fallback():
     """The fallback path of xec_decode's uploads (the caller's scratch, on the
     stream) -- taken when no library buffer can be had, forced here with

@@ -8,7 +8,8 @@
 // cost), xec_encode + stream sync, xec_encode + event sync, a captured
 // hipGraph holding the encode + graph sync, and xec_decode (one lost data
 // block per stripe, pinned host bitmap) + stream sync with the automatic and
-// the work-list tiling.
+// the work-list tiling; and xec_decode of a batch without losses, alone and
+// + stream sync.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -167,5 +168,18 @@ int main(int argc, char** argv) {
     t.clear();
   }
   xec_set_decode_tiling(0);
+  // decode of a batch without losses (the reference's lost=0 rows): the host
+  // scan finds nothing, so nothing is queued; alone and + stream sync
+  for (size_t i = 0; i < S * (k + m); ++i) h_bm[i] = 1;
+  for (int sync : {0, 1}) {
+    for (int i = 0; i < iters + 50; ++i) {
+      auto t0 = clk::now();
+      if (xec_decode(d, p, S, bs, k, m, h_bm, d_bm, s) != XEC_SUCCESS) return 2;
+      if (sync) CK(hipStreamSynchronize(s));
+      if (i >= 50) t.push_back(us_since(t0));
+    }
+    report(sync ? "xec_decode no loss + sync" : "xec_decode no loss", t);
+    t.clear();
+  }
   return 0;
 }
