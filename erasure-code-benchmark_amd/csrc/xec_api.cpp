@@ -461,12 +461,19 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   }
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
-  const bool side = side_uploads() && stream_busy(stream);
+  // Whether uploads go off the stream, asked (hipStreamQuery) only when
+  // something is about to be uploaded: a list that travels in the kernel
+  // arguments never pays for the query.
+  int side_state = -1;
+  auto side = [&]() {
+    if (side_state < 0) side_state = side_uploads() && stream_busy(stream) ? 1 : 0;
+    return side_state == 1;
+  };
   // The bitmap goes to the device (a library buffer, or the caller's scratch
   // on `stream`); for large bitmaps before the scan, so the two overlap.
   Upload bmu;
   auto upload_bitmap = [&]() -> bool {
-    if (side && upload_begin(h_bitmap, bitmap_bytes, dev, bmu)) return true;
+    if (side() && upload_begin(h_bitmap, bitmap_bytes, dev, bmu)) return true;
     bmu = Upload{};
     bmu.dev = d_bitmap;
     return hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice, stream) ==
@@ -513,7 +520,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
     const uint64_t cap = bitmap_bytes > pad ? (bitmap_bytes - pad) / 4 : 0;
     const uint64_t n = scan.lost_data;
     Staging* sg = nullptr;
-    if (side || n <= cap) sg = stage_acquire(n * 4, dev);
+    if (side() || n <= cap) sg = stage_acquire(n * 4, dev);
     if (sg != nullptr) {
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, static_cast<uint32_t*>(sg->host), n);
       if (st != XEC_SUCCESS) {
@@ -523,7 +530,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
       }
       Upload lu;
       bool ok = true;
-      if (side && upload_begin(sg->host, n * 4, dev, lu)) {
+      if (side() && upload_begin(sg->host, n * 4, dev, lu)) {
         stage_release(sg, true, lu.cs);
         ok = upload_join(lu, stream);
       } else if (n <= cap) {

@@ -168,6 +168,17 @@ int main(int argc, char** argv) {
     t.clear();
   }
   xec_set_decode_tiling(0);
+  // the host time of the decode call alone (its stream synchronised outside
+  // the timed region): what a caller that does not wait pays per call
+  for (int i = 0; i < iters + 50; ++i) {
+    auto t0 = clk::now();
+    if (xec_decode(d, p, S, bs, k, m, h_bm, d_bm, s) != XEC_SUCCESS) return 2;
+    const double us = us_since(t0);
+    CK(hipStreamSynchronize(s));
+    if (i >= 50) t.push_back(us);
+  }
+  report("xec_decode auto, call only", t);
+  t.clear();
   // decode of a batch without losses (the reference's lost=0 rows): the host
   // scan finds nothing, so nothing is queued; alone and + stream sync
   for (size_t i = 0; i < S * (k + m); ++i) h_bm[i] = 1;
