@@ -126,49 +126,66 @@ constexpr size_t kMaxStaging = 64;
 std::mutex g_stage_mu;
 std::vector<Staging*> g_stage;
 
+// hipEventQuery on a buffer's event: true once the work it marks has passed.
+// Only hipErrorNotReady means "not yet"; it is cleared so that no later
+// hipGetLastError reads it as a launch failure.  Any other error is left for
+// the caller to read and the buffer counts as in use.
+bool event_passed(hipEvent_t e) {
+  const hipError_t q = hipEventQuery(e);
+  if (q == hipErrorNotReady) (void)hipGetLastError();
+  return q == hipSuccess;
+}
+
+// The slot is picked and marked busy under the lock; waiting for a recycled
+// buffer's last reader and re-allocating happen after the lock is dropped, so
+// one thread waiting for another's copy never stalls other threads' calls.
 Staging* stage_acquire(size_t bytes, int dev) {
-  std::unique_lock<std::mutex> lk(g_stage_mu);
   Staging* pick = nullptr;
-  for (Staging* st : g_stage) {
-    if (st->busy || st->device != dev || st->cap < bytes) continue;
-    if (hipEventQuery(st->done) != hipSuccess) continue;  // a queued copy still reads it
-    if (pick == nullptr || st->cap < pick->cap) pick = st;
-  }
-  if (pick == nullptr && g_stage.size() >= kMaxStaging) {
-    for (Staging* st : g_stage)  // recycle an idle one of this device: wait for its copy
-      if (!st->busy && st->device == dev) {
-        pick = st;
-        break;
-      }
-    if (pick != nullptr) {
-      if (hipEventSynchronize(pick->done) != hipSuccess) return nullptr;
-      if (pick->cap < bytes) {
-        (void)hipHostFree(pick->host);
-        pick->host = nullptr;
-        pick->cap = 0;
-      }
+  bool recycled = false;
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    for (Staging* st : g_stage) {
+      if (st->busy || st->device != dev || st->cap < bytes) continue;
+      if (!event_passed(st->done)) continue;  // a queued copy still reads it
+      if (pick == nullptr || st->cap < pick->cap) pick = st;
     }
-  }
-  if (pick == nullptr) {
-    pick = new Staging;
-    pick->device = dev;
-    if (hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {
-      delete pick;
-      return nullptr;
+    if (pick == nullptr && g_stage.size() >= kMaxStaging) {
+      for (Staging* st : g_stage)  // recycle an idle one of this device: wait for its copy
+        if (!st->busy && st->device == dev) {
+          pick = st;
+          recycled = true;
+          break;
+        }
     }
-    g_stage.push_back(pick);
+    if (pick == nullptr) {
+      pick = new Staging;
+      pick->device = dev;
+      if (hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {
+        delete pick;
+        return nullptr;
+      }
+      g_stage.push_back(pick);
+    }
+    pick->busy = true;
   }
+  auto give_back = [&]() {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    pick->busy = false;
+    return nullptr;
+  };
+  if (recycled && hipEventSynchronize(pick->done) != hipSuccess) return give_back();
   if (pick->cap < bytes) {
+    if (pick->host != nullptr) (void)hipHostFree(pick->host);
+    pick->host = nullptr;
+    pick->cap = 0;
     size_t cap = 64u << 10;
     while (cap < bytes) cap <<= 1;
     if (hipHostMalloc(&pick->host, cap, hipHostMallocDefault) != hipSuccess) {
       pick->host = nullptr;
-      pick->cap = 0;
-      return nullptr;
+      return give_back();
     }
     pick->cap = cap;
   }
-  pick->busy = true;
   return pick;
 }
 
@@ -243,13 +260,45 @@ bool side_uploads() {
 // add latency: 8 MiB (40/32) with 8 lost ran at 2,284 instead of 3,669
 // Gbit/s per call, 128 MiB with 2-8 lost 21-27 % slower (tools/ab/
 // refrows_ab.sh, profiles/r03zk).  A NotReady answer is cleared so that no
-// later hipGetLastError reads it as a launch failure.
-bool stream_busy(hipStream_t stream) {
+// later hipGetLastError reads it as a launch failure; any other answer (a
+// sticky fault of earlier work, an invalid stream) is an error the caller
+// gets back as XEC_DEVICE_ERROR, and is left for its hipGetLastError.
+// Returns 0 idle, 1 busy, -1 error.
+int stream_busy(hipStream_t stream) {
   const hipError_t q = hipStreamQuery(stream);
-  if (q == hipSuccess) return false;
+  if (q == hipSuccess) return 0;
+  if (q != hipErrorNotReady) return -1;
   (void)hipGetLastError();
-  return true;
+  return 1;
 }
+
+// The device `stream` belongs to (the current device for the null stream).
+// HIP accepts a stream of device B while device A is current, and the decode
+// kernel then runs on B: the library buffers, copy stream and staging the
+// call uses must be B's too.  So a decode makes the stream's device current
+// for its duration and restores the caller's on return.
+class StreamDevice {
+ public:
+  explicit StreamDevice(hipStream_t stream) {
+    ok_ = hipGetDevice(&prev_) == hipSuccess;
+    dev_ = prev_;
+    if (ok_ && stream != nullptr) {
+      ok_ = hipStreamGetDevice(stream, &dev_) == hipSuccess;
+      if (ok_ && dev_ != prev_) ok_ = switched_ = hipSetDevice(dev_) == hipSuccess;
+    }
+  }
+  ~StreamDevice() {
+    if (switched_) (void)hipSetDevice(prev_);
+  }
+  StreamDevice(const StreamDevice&) = delete;
+  StreamDevice& operator=(const StreamDevice&) = delete;
+  bool ok() const { return ok_; }
+  int device() const { return dev_; }
+
+ private:
+  int prev_ = 0, dev_ = 0;
+  bool ok_ = false, switched_ = false;
+};
 
 bool capturing(hipStream_t stream) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -258,33 +307,32 @@ bool capturing(hipStream_t stream) {
 
 // Starts copying `bytes` of host memory to a library buffer on the device's
 // copy stream; false (nothing queued) if no buffer or stream can be had.
+// `dev` is the current device (StreamDevice).  As in stage_acquire, a slot is
+// picked and marked busy under the lock, and a recycled slot's wait and
+// re-allocation happen outside it.
 bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
   DevSlot* pick = nullptr;
   hipStream_t cs = nullptr;
+  bool recycled = false;
   {
     std::lock_guard<std::mutex> lk(g_slot_mu);
     cs = copy_stream(dev);
     if (cs == nullptr) return false;
     for (DevSlot* sl : g_slots) {
       if (sl->busy || sl->device != dev || sl->cap < bytes) continue;
-      if (hipEventQuery(sl->done) != hipSuccess) continue;  // a kernel still reads it
+      if (!event_passed(sl->done)) continue;  // a kernel still reads it
       if (pick == nullptr || sl->cap < pick->cap) pick = sl;
     }
     size_t mine = 0;
     for (DevSlot* sl : g_slots) mine += sl->device == dev;
     if (pick == nullptr && mine >= kMaxSlots) {
-      for (DevSlot* sl : g_slots)  // recycle an idle one: wait for its reader
+      for (DevSlot* sl : g_slots)  // recycle an idle one: wait for its reader (below)
         if (!sl->busy && sl->device == dev) {
           pick = sl;
+          recycled = true;
           break;
         }
       if (pick == nullptr) return false;
-      if (hipEventSynchronize(pick->done) != hipSuccess) return false;
-      if (pick->cap < bytes) {
-        (void)hipFree(pick->dev);
-        pick->dev = nullptr;
-        pick->cap = 0;
-      }
     }
     if (pick == nullptr) {
       pick = new DevSlot;
@@ -299,15 +347,21 @@ bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
     }
     pick->busy = true;
   }
+  auto give_back = [&]() {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    pick->busy = false;
+    return false;
+  };
+  if (recycled && hipEventSynchronize(pick->done) != hipSuccess) return give_back();
   if (pick->cap < bytes) {
+    if (pick->dev != nullptr) (void)hipFree(pick->dev);
+    pick->dev = nullptr;
+    pick->cap = 0;
     size_t cap = 64u << 10;
     while (cap < bytes) cap <<= 1;
     if (hipMalloc(&pick->dev, cap) != hipSuccess) {
       pick->dev = nullptr;
-      pick->cap = 0;
-      std::lock_guard<std::mutex> lk(g_slot_mu);
-      pick->busy = false;
-      return false;
+      return give_back();
     }
     pick->cap = cap;
   }
@@ -459,14 +513,20 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
     if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) return st;
     if (cap || capturing(stream)) return XEC_DEVICE_ERROR;
   }
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
+  const StreamDevice sd(stream);
+  if (!sd.ok()) return XEC_DEVICE_ERROR;
+  const int dev = sd.device();
   // Whether uploads go off the stream, asked (hipStreamQuery) only when
   // something is about to be uploaded: a list that travels in the kernel
-  // arguments never pays for the query.
-  int side_state = -1;
+  // arguments never pays for the query.  A query that fails (not merely
+  // "busy") fails the call.
+  int side_state = -2;
+  bool query_failed = false;
   auto side = [&]() {
-    if (side_state < 0) side_state = side_uploads() && stream_busy(stream) ? 1 : 0;
+    if (side_state == -2) {
+      side_state = side_uploads() ? stream_busy(stream) : 0;
+      query_failed = side_state < 0;
+    }
     return side_state == 1;
   };
   // The bitmap goes to the device (a library buffer, or the caller's scratch
@@ -474,6 +534,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   Upload bmu;
   auto upload_bitmap = [&]() -> bool {
     if (side() && upload_begin(h_bitmap, bitmap_bytes, dev, bmu)) return true;
+    if (query_failed) return false;
     bmu = Upload{};
     bmu.dev = d_bitmap;
     return hipMemcpyAsync(d_bitmap, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice, stream) ==
@@ -520,7 +581,12 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
     const uint64_t cap = bitmap_bytes > pad ? (bitmap_bytes - pad) / 4 : 0;
     const uint64_t n = scan.lost_data;
     Staging* sg = nullptr;
-    if (side() || n <= cap) sg = stage_acquire(n * 4, dev);
+    const bool off_stream = side();
+    if (query_failed) {
+      upload_end(bmu, stream, false);
+      return XEC_DEVICE_ERROR;
+    }
+    if (off_stream || n <= cap) sg = stage_acquire(n * 4, dev);
     if (sg != nullptr) {
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, static_cast<uint32_t*>(sg->host), n);
       if (st != XEC_SUCCESS) {
@@ -613,15 +679,18 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
   // goes through the scratch in pieces of what it holds: copy a piece, rebuild
   // it, copy the next (stream order keeps a copy behind the kernel still
   // reading the previous piece).
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
+  const StreamDevice sd(stream);  // the stream's device, as in xec_decode
+  if (!sd.ok()) return XEC_DEVICE_ERROR;
+  const int dev = sd.device();
+  const int busy = side_uploads() ? stream_busy(stream) : 0;
+  if (busy < 0) return XEC_DEVICE_ERROR;
   Staging* sg = stage_acquire(n * 4, dev);
   if (sg == nullptr) return XEC_DEVICE_ERROR;
   uint32_t* items = static_cast<uint32_t*>(sg->host);
   (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, n, &n, &failures);
   g_tiling_used = XEC_TILING_LIST;
   Upload lu;
-  if (side_uploads() && stream_busy(stream) && upload_begin(items, n * 4, dev, lu)) {
+  if (busy == 1 && upload_begin(items, n * 4, dev, lu)) {
     stage_release(sg, true, lu.cs);
     const bool ok = upload_join(lu, stream) &&
                     xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,
@@ -705,7 +774,10 @@ xec_status xec_decode_device_list(void* d_data, const void* d_parity, size_t S, 
     return hipMemsetAsync(d_status, 0, sizeof(int32_t), stream) == hipSuccess ? XEC_SUCCESS
                                                                               : XEC_DEVICE_ERROR;
   // one reduction per tile, as encode: encode's residency table; the grid is
-  // what the chip holds at once unless xec_set_launch gave max_grid
+  // what the chip holds at once (on the stream's device) unless xec_set_launch
+  // gave max_grid
+  const StreamDevice sd(stream);
+  if (!sd.ok()) return XEC_DEVICE_ERROR;
   xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
   if (ls.max_grid == 0) ls.max_grid = resident_workgroups(ls);
   if (ls.max_grid == 0) return XEC_DEVICE_ERROR;
@@ -788,6 +860,44 @@ xec_status xec_set_decode_tiling(int tiling) {
 xec_status xec_set_validate_kernel(int mode) {
   if (mode < 0 || mode > 2) return XEC_INVALID_SIZE;
   xec::g_validate_mode = mode;
+  return XEC_SUCCESS;
+}
+
+xec_status xec_get_tuning(xec_tuning* out) {
+  if (out == nullptr) return XEC_INVALID_ALIGNMENT;
+  out->unroll = g_unroll;
+  out->max_grid = g_max_grid;
+  out->cache_policy = g_nt;
+  out->block_threads = g_threads;
+  out->waves_per_simd = g_occupancy;
+  out->decode_tiling = g_decode_tiling;
+  out->validate_kernel = xec::g_validate_mode;
+  return XEC_SUCCESS;
+}
+
+xec_status xec_set_tuning(const xec_tuning* in) {
+  if (in == nullptr) return XEC_INVALID_ALIGNMENT;
+  // all or nothing: each setter checks its own fields; if any rejects, the
+  // thread's previous values are put back
+  const xec_tuning keep = [] {
+    xec_tuning t{};
+    (void)xec_get_tuning(&t);
+    return t;
+  }();
+  if (xec_set_launch(in->unroll, in->max_grid, in->cache_policy, in->block_threads) !=
+          XEC_SUCCESS ||
+      xec_set_occupancy(in->waves_per_simd) != XEC_SUCCESS ||
+      xec_set_decode_tiling(in->decode_tiling) != XEC_SUCCESS ||
+      xec_set_validate_kernel(in->validate_kernel) != XEC_SUCCESS) {
+    g_unroll = keep.unroll;
+    g_max_grid = keep.max_grid;
+    g_nt = keep.cache_policy;
+    g_threads = keep.block_threads;
+    g_occupancy = keep.waves_per_simd;
+    g_decode_tiling = keep.decode_tiling;
+    xec::g_validate_mode = keep.validate_kernel;
+    return XEC_INVALID_SIZE;
+  }
   return XEC_SUCCESS;
 }
 

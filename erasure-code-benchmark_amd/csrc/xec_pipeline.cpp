@@ -154,8 +154,12 @@ void destroy_slots(xec_pipeline* p) {
 
 // Whether the host buffer at q is pinned (page-locked and known to HIP).
 // Pageable memory is not registered and hipPointerGetAttributes fails on it;
-// the error is cleared so it cannot surface in a later hipGetLastError.
+// that error -- ours -- is cleared so it cannot surface in a later
+// hipGetLastError.  An error the caller has not read yet stays the caller's:
+// with one pending the query is skipped and the buffer is treated as pageable
+// (the bounce path, correct for any host memory), so nothing is cleared.
 bool host_pinned(const void* q) {
+  if (hipPeekAtLastError() != hipSuccess) return false;
   hipPointerAttribute_t a{};
   if (hipPointerGetAttributes(&a, q) != hipSuccess) {
     (void)hipGetLastError();

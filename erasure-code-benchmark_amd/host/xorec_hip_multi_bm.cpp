@@ -146,13 +146,22 @@ int XorecBenchmarkHipMulti::encode() noexcept {
 // on the device count.  Otherwise every shard decodes its slice (xec_decode:
 // host scan, then the launch) on its own thread, so no device's launch waits
 // for another's scan; then every stream is waited for.
+// The library's tuning overrides are per thread (include/xec.h): the caller's
+// are copied into every worker before its xec_decode, so all shards launch the
+// shape the caller configured, not the workers' defaults.
 int XorecBenchmarkHipMulti::decode() noexcept {
   const size_t n = m_shards.size();
   std::vector<int> st(n, XEC_DEVICE_ERROR);
   Rendezvous all_recoverable(n);
   bool launched = false;  // every shard reached xec_decode (written by shard 0)
+  xec_tuning tuning{};
+  const bool tuned = xec_get_tuning(&tuning) == XEC_SUCCESS;
   m_pool->run([&](size_t i) {
     const Shard& s = m_shards[i];
+    if (i != 0 && (!tuned || xec_set_tuning(&tuning) != XEC_SUCCESS)) {
+      (void)all_recoverable.arrive(false);  // the others must not wait for this shard
+      return;                               // st[i] stays XEC_DEVICE_ERROR
+    }
     const uint8_t* bm = m_block_bitmap.get() + s.first * m_chunk_tot_blocks;
     int needs = 0;
     const int check = xec_check_bitmap(bm, s.count, m_chunk_data_blocks, m_chunk_parity_blocks,

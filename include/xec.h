@@ -252,6 +252,22 @@ xec_status xec_set_decode_tiling(int tiling);
  * identical.  XEC_INVALID_SIZE outside 0..2. */
 xec_status xec_set_validate_kernel(int mode);
 
+/* The calling thread's overrides above as one value.  A caller that fans its
+ * calls out to threads of its own (XorecBenchmarkHipMulti's shard workers)
+ * reads them with xec_get_tuning and applies them in each worker with
+ * xec_set_tuning, so every thread launches the shape the caller configured.
+ * xec_set_tuning checks every field as the setters do and changes nothing
+ * unless all are valid (XEC_INVALID_SIZE); a null pointer is
+ * XEC_INVALID_ALIGNMENT. */
+typedef struct {
+  int unroll, max_grid, cache_policy, block_threads; /* xec_set_launch */
+  int waves_per_simd;                                /* xec_set_occupancy */
+  int decode_tiling;                                 /* xec_set_decode_tiling */
+  int validate_kernel;                               /* xec_set_validate_kernel */
+} xec_tuning;
+xec_status xec_get_tuning(xec_tuning* out);
+xec_status xec_set_tuning(const xec_tuning* in);
+
 /* Diagnostics: which tiling the calling thread's most recent xec_decode
  * launched -- 0 none (an error, or nothing to rebuild), then one of: */
 enum {

@@ -51,16 +51,16 @@ def gpu():
 
 
 def run_tsan(cmd, **kw):
-    """Run a ThreadSanitizer binary.  On kernels with high mmap randomisation
-    TSan can abort at start-up ("FATAL: ThreadSanitizer: unexpected memory
-    mapping", seen on one GPU box) before any test code runs; the run is then
-    repeated once with address-space randomisation off for that process
-    (`setarch -R`, which starts the binary before it touches any device)."""
+    """Run a ThreadSanitizer binary, always with address-space randomisation
+    off for that process (`setarch <arch> -R`), from the first attempt and with
+    no retry.  TSan's fixed shadow layout clashes with high mmap randomisation
+    ("FATAL: ThreadSanitizer: unexpected memory mapping", seen once on a GPU
+    box); setarch runs in a fresh child, before the binary touches any device,
+    so nothing execs from a process that has initialised the GPU.  Any abort
+    now fails the test instead of being retried away."""
     import platform
     import subprocess
-    p = subprocess.run(cmd, capture_output=True, text=True, **kw)
-    if p.returncode != 0 and "unexpected memory mapping" in p.stderr:
-        p = subprocess.run(["setarch", platform.machine(), "-R", *map(str, cmd)],
-                           capture_output=True, text=True, **kw)
-    return p
+    full = ["setarch", platform.machine(), "-R", *map(str, cmd)]
+    print(f"run_tsan: ASLR off for the TSan run: {' '.join(full)}")
+    return subprocess.run(full, capture_output=True, text=True, **kw)
 

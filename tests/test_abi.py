@@ -169,6 +169,47 @@ def test_set_occupancy_validation():
         assert xec.set_occupancy(w) == xec.Status.SUCCESS
 
 
+def test_tuning_snapshot_roundtrip_and_all_or_nothing():
+    """xec_get_tuning / xec_set_tuning (the multi-device plugin's
+    workers take the caller's overrides): a snapshot round-trips, an invalid
+    field changes nothing, and another thread starts at the defaults."""
+    import ctypes
+    import threading
+    from xec._lib import Tuning
+    L = xec.lib()
+    t = Tuning()
+    try:
+        assert xec.set_launch(2, 64, 1, 256) == xec.Status.SUCCESS
+        assert xec.set_occupancy(4) == xec.Status.SUCCESS
+        assert L.xec_set_decode_tiling(3) == 0 and L.xec_set_validate_kernel(1) == 0
+        assert L.xec_get_tuning(ctypes.byref(t)) == 0
+        assert (t.unroll, t.max_grid, t.cache_policy, t.block_threads, t.waves_per_simd,
+                t.decode_tiling, t.validate_kernel) == (2, 64, 1, 256, 4, 3, 1)
+        seen = {}
+
+        def worker():
+            w = Tuning()
+            L.xec_get_tuning(ctypes.byref(w))
+            seen["fresh"] = (w.unroll, w.decode_tiling, w.validate_kernel)
+            seen["set"] = L.xec_set_tuning(ctypes.byref(t))
+            L.xec_get_tuning(ctypes.byref(w))
+            seen["after"] = (w.unroll, w.max_grid, w.decode_tiling, w.validate_kernel)
+
+        th = threading.Thread(target=worker)
+        th.start()
+        th.join()
+        assert seen == {"fresh": (0, 0, 0), "set": 0, "after": (2, 64, 3, 1)}
+        bad = Tuning(1, 0, 0, 64, 0, 7, 0)  # decode_tiling 7 is invalid
+        assert L.xec_set_tuning(ctypes.byref(bad)) == xec.Status.INVALID_SIZE
+        u = Tuning()
+        L.xec_get_tuning(ctypes.byref(u))
+        assert (u.unroll, u.max_grid, u.block_threads, u.decode_tiling) == (2, 64, 256, 3)
+        assert L.xec_get_tuning(None) == xec.Status.INVALID_ALIGNMENT
+        assert L.xec_set_tuning(None) == xec.Status.INVALID_ALIGNMENT
+    finally:
+        assert L.xec_set_tuning(ctypes.byref(Tuning())) == 0  # back to the defaults
+
+
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
 def test_header_is_plain_c_and_links(tmp_path):
     """The boundary is a C ABI: include/xec.h compiles as strict C99 (no C++,
