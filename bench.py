@@ -99,6 +99,12 @@ def parse():
                          "a test can make the legs' watchdog fire deterministically")
     ap.add_argument("--rank-grace", type=float, default=60.0,
                     help="launcher: seconds to wait for the other ranks after one fails")
+    ap.add_argument("--multi-devices", default="",
+                    help="the multi_device leg's device list (comma separated, repeats allowed: "
+                         "0,0 rehearses it on one GPU); default at N>1: the N devices the ranks "
+                         "ran on; 'none' skips it")
+    ap.add_argument("--multi-timeout", type=float, default=300.0,
+                    help="seconds before the multi_device leg's child process is killed")
     return ap.parse_args()
 
 
@@ -445,6 +451,62 @@ def measure_host_pipeline(torch, dist, xec, k, m, bs, S, start, coll_dev, reps=3
     pl.close()
     return (t_enc, t_dec, ok, (f"xec_pipeline status {sorted(set(rcs))}" if any(rcs) else None),
             numa)
+
+
+MULTI_LEG_BIN = ROOT / "erasure-code-benchmark_amd" / "bin" / "xec_multi_leg"
+
+
+def multi_device_list(args, world, ndev):
+    """The multi_device leg's devices: --multi-devices, else at N > 1 the N
+    devices the ranks ran on (rank r on device r % visible, as run_rank picks
+    them); None when the leg is off (N = 1 without the flag, or 'none')."""
+    spec = args.multi_devices.strip().lower()
+    if spec == "none":
+        return None
+    if spec:
+        return [int(x) for x in spec.split(",")]
+    if world > 1:
+        return [r % ndev for r in range(world)]
+    return None
+
+
+def run_multi_device_leg(args, devices, k, m, bs, S_per):
+    """Config 5 through the ONE-process multi-device plugin:
+    XorecBenchmarkHipMulti over `devices` -- device-resident encode + decode
+    timed from first launch to last completion, validated, then the batch
+    scattered from the root's HBM with hipMemcpyPeerAsync, encoded per shard
+    and the parity gathered back and compared with the root's own encode
+    (host/xec_multi_leg.cpp).  Runs as a fresh child process started after
+    every rank has finished its GPU work, under its own time limit: a stuck
+    peer copy costs this field, never the line.  With --rehearse-cpu the child
+    is the CPU stand-in (tools/cpu_rehearsal.py multi-leg)."""
+    import subprocess
+    leg_args = ["--devices", ",".join(map(str, devices)), "--stripes-per-device", str(S_per),
+                "--data", str(k), "--parity", str(m), "--block", str(bs)]
+    if args.rehearse_cpu:
+        cmd = [sys.executable, str(ROOT / "tools" / "cpu_rehearsal.py"), "multi-leg", *leg_args]
+    else:
+        if not MULTI_LEG_BIN.exists():
+            return {"error": f"{MULTI_LEG_BIN.relative_to(ROOT)} not built (make -C "
+                             "erasure-code-benchmark_amd)"}
+        cmd = [str(MULTI_LEG_BIN), *leg_args]
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=args.multi_timeout,
+                           cwd=str(ROOT))
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out ({args.multi_timeout:.0f} s): child killed",
+                "devices": devices}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    try:
+        res = json.loads(lines[-1])
+    except (IndexError, ValueError):
+        res = {"error": f"exit {p.returncode}, no result line; stderr: {p.stderr[-300:]}"}
+    if p.returncode != 0 and "error" not in res:
+        res["error"] = f"exit {p.returncode} (a check failed: see bit_exact / scatter)"
+    res["child_wall_s"] = round(time.perf_counter() - t0, 2)
+    res["command"] = " ".join([Path(cmd[0]).name, *cmd[1:]])
+    return res
 
 
 def launch_ranks(n, argv, grace_s):
@@ -925,9 +987,31 @@ def run_rank(args):
             except Exception as e:  # noqa: BLE001 - report, keep the headline line
                 sc = {"error": repr(e)[:200]}
             merge("scatter", sc)
-        dog.cancel()
         with lock:
             printed.append(True)  # a watchdog firing from here on finds the legs done
+        dog.cancel()
+
+    # The multi_device leg (N > 1, or --multi-devices): a child process that
+    # opens every device itself, started by rank 0 once all ranks have freed
+    # their buffers and met; the other ranks leave first, so no rank's
+    # collective kernel spins on a GPU while the child measures.
+    multi = None if bad else multi_device_list(args, world, ndev)
+    if multi is not None:
+        del sets, scratch, d_bm, d_status, events
+        if devname == "cuda":
+            cuda.synchronize()
+            torch.cuda.empty_cache()
+        if use_dist:
+            dist.barrier()
+            if rank != 0:
+                dist.destroy_process_group()
+                return
+        with markers.region("bench:multi_device"):
+            out["multi_device"] = run_multi_device_leg(args, multi, k, m, bs, S_per)
+        print(json.dumps(out), file=result_out, flush=True)
+        if use_dist:
+            dist.destroy_process_group()
+        return
     if out is not None:
         print(json.dumps(out), file=result_out, flush=True)
     if use_dist:

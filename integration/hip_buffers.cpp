@@ -44,4 +44,34 @@ void destroy_stream(hipStream_t stream) {
   if (stream) (void)hipStreamDestroy(stream);
 }
 
+int device_count() {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+int current_device() {
+  int d = -1;
+  return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
+
+bool set_device(int device) { return hipSetDevice(device) == hipSuccess; }
+
+bool enable_peer_access(int device, int peer) {
+  if (device == peer) return true;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess) return false;
+  if (!can) return true;  // the runtime stages such copies itself
+  const int prev = current_device();
+  if (hipSetDevice(device) != hipSuccess) return false;
+  const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();  // ours: clear it
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+}
+
+bool copy_peer(void* dst, int dst_device, const void* src, int src_device, size_t bytes,
+               hipStream_t stream) {
+  return hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, stream) == hipSuccess;
+}
+
 }  // namespace xec_hip

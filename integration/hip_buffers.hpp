@@ -34,6 +34,21 @@ bool synchronize(hipStream_t stream);
 hipStream_t create_stream();
 void destroy_stream(hipStream_t stream);
 
+// Devices (XorecBenchmarkHipMulti): the visible count (0 on failure), the
+// current device (-1 on failure) and making one current; true on success.
+int device_count();
+int current_device();
+bool set_device(int device);
+
+// `device` gets access to `peer`'s memory where the pair supports it (an
+// access already enabled is fine); true unless a runtime call failed.
+bool enable_peer_access(int device, int peer);
+
+// Stream-ordered copy between two devices' memory (xGMI DMA between GPUs, a
+// device copy when both are the same device); true on success.
+bool copy_peer(void* dst, int dst_device, const void* src, int src_device, size_t bytes,
+               hipStream_t stream);
+
 }  // namespace xec_hip
 
 #endif  // XEC_INTEGRATION_HIP_BUFFERS_HPP

@@ -1,0 +1,82 @@
+// xorec_hip_multi_bm.hpp -- the MI355X XOR-EC plugin over SEVERAL GPUs of one
+// node in one process (BASELINE.json configs[4]), written against the
+// reference's UNMODIFIED plugin interface (src/algorithms/abstract_bm.hpp:18-88,
+// src/benchmark/bm_config.hpp:25-43) as a maintainer would add it to
+// src/algorithms/ next to XorecBenchmarkGpuCmp (xorec_gpu_cmp_bm.hpp:1-23).
+//
+// BenchmarkConfig is used as the reference defines it: no new field.  The
+// devices come from the environment variable XEC_DEVICES (comma-separated
+// HIP device ids, repeats allowed: "0,0" cuts the batch into two slices on
+// one GPU), else every visible device.
+//
+// The batch's stripes are cut into contiguous ranges, one per device (stripes
+// are independent: xorec_bm.cpp:30, xorec_gpu_cmp.cu:135-144), each range's
+// data / parity / scratch in its device's HBM, each device with its own
+// stream; a stripe sits at the same offset inside its range as in one
+// buffer.  encode() / decode() launch on every device, then wait for all, so
+// BM_generic's clock (abstract_runner.hpp:104-112) spans first launch to last
+// completion.  decode() is all-or-nothing over the WHOLE batch, as the
+// reference's GPU decode (xorec_gpu_cmp.cu:75-81): every range's bitmap is
+// checked (xec_check_bitmap) before any device launches.
+//
+// The codec is libxec_hip.so's C ABI (include/xec.h); HIP allocations and
+// copies go through hip_buffers.hpp.  tests/test_reference_integration.py
+// compiles this file with the reference's own abstract_bm.cpp and utils.cpp
+// and links it against libxec_hip.so.
+#ifndef XOREC_HIP_MULTI_BM_HPP
+#define XOREC_HIP_MULTI_BM_HPP
+
+#include <vector>
+
+#include "abstract_bm.hpp"
+#include "xec.h"
+
+class XorecBenchmarkHipMulti : public AbstractBenchmark {
+public:
+  explicit XorecBenchmarkHipMulti(const BenchmarkConfig& config);
+  ~XorecBenchmarkHipMulti() noexcept override;
+  XorecBenchmarkHipMulti(const XorecBenchmarkHipMulti&) = delete;
+  XorecBenchmarkHipMulti& operator=(const XorecBenchmarkHipMulti&) = delete;
+
+  void setup() noexcept override;
+  int encode() noexcept override;
+  int decode() noexcept override;
+  void simulate_data_loss() noexcept override;
+  bool check_for_corruption() const noexcept override;
+
+  // Config 5's exchange (no reference counterpart: the reference is one GPU):
+  // the batch starts in `root`'s HBM (the reference layout, m_chunks stripes)
+  // and each range is copied to its device over xGMI; gather_parity_to is the
+  // inverse for the parity.  Return when every copy has landed; 0 or -1.
+  int scatter_from(const uint8_t* d_root_data, int root) noexcept;
+  int gather_parity_to(uint8_t* d_root_parity, int root) noexcept;
+
+  size_t num_shards() const noexcept { return m_shards.size(); }
+
+protected:
+  void m_write_data_buffer() noexcept override;
+
+private:
+  using DevBuf = std::unique_ptr<uint8_t[], DeleterFunc<uint8_t>>;
+  struct Shard {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    size_t first = 0, count = 0;  ///< global stripe range
+    DevBuf data{nullptr, nullptr};      ///< count * k * bs
+    DevBuf parity{nullptr, nullptr};    ///< count * m * bs
+    DevBuf d_bitmap{nullptr, nullptr};  ///< xec_decode scratch, count * (k + m)
+    DevBuf d_erase{nullptr, nullptr};   ///< device copy of the erasure bitmap slice
+    DevBuf d_bad{nullptr, nullptr};     ///< device count of invalid blocks
+  };
+
+  // Runs fn(shard) on every shard with its device current, then waits for
+  // every stream; false if any call or wait failed.  The caller's current
+  // device is restored.
+  template <typename F>
+  bool each(F&& fn) const noexcept;
+  bool enable_peers(int root) const noexcept;
+
+  std::vector<Shard> m_shards;
+};
+
+#endif  // XOREC_HIP_MULTI_BM_HPP

@@ -46,6 +46,14 @@ def test_launcher_plain_command(n):
     assert sc["bit_exact"] is True and sc["gathered_parity_bit_exact_vs_root_encode"] is True
     # max-over-ranks: the reported step time covers every rank's elapsed time
     assert out["ms_per_step"] * out["steps"] >= max(r["elapsed_ms"] for r in out["per_rank"]) - 1e-3
+    # the one-process multi-device leg: a child started by
+    # rank 0 after every rank finished, over the N devices the ranks ran on
+    md = out["multi_device"]
+    assert md["rehearsal"] is True and md["devices"] == [0] * n  # CPU stand-ins: one "device"
+    assert md["stripes_per_device"] == 5 and md["stripes_total"] == 5 * n
+    assert md["bit_exact"] is True
+    assert md["scatter"]["gathered_parity_bit_exact_vs_root_encode"] is True
+    assert "error" not in md
 
 
 def test_torchrun_launch_one_line():
@@ -66,6 +74,38 @@ def test_torchrun_launch_one_line():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 4 and out["dist"]["ranks_seen"] == 4
     assert out["dist"]["launcher"] == "external"
+    # under an external launcher rank 0 starts the multi-device leg itself
+    assert out["multi_device"]["bit_exact"] is True and out["multi_device"]["devices"] == [0] * 4
+
+
+def test_multi_device_leg_at_n1_with_a_device_list():
+    """--multi-devices 0,0 runs the leg at N=1 (how a one-GPU box rehearses
+    config 5's plugin with a repeated device list); still one stdout line."""
+    p = _bench("--rehearse-cpu", "--dist-backend", "gloo", "--workload", "4,1,4096,3",
+               "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--multi-devices", "0,0")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
+    md = json.loads(lines[0])["multi_device"]
+    assert md["devices"] == [0, 0] and md["bit_exact"] is True and md["stripes_total"] == 6
+
+
+def test_multi_device_leg_timeout_costs_the_field_not_the_line():
+    p = _bench("--gpus", "2", "--rehearse-cpu", "--dist-backend", "gloo", "--workload",
+               "8,2,4096,5", "--steps", "2", "--warmup", "1", "--multi-timeout", "0.01")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert "timed out" in out["multi_device"]["error"]
+    assert out["verified"] is True and out["value"] > 0
+
+
+def test_multi_device_leg_off():
+    p = _bench("--gpus", "2", "--rehearse-cpu", "--dist-backend", "gloo", "--workload",
+               "8,2,4096,5", "--steps", "2", "--warmup", "1", "--multi-devices", "none")
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "multi_device" not in json.loads(p.stdout.strip())
 
 
 def test_launcher_propagates_rank_failure():

@@ -1,7 +1,9 @@
-"""The reference-side plugin against the reference's UNMODIFIED plugin interface.
+"""The reference-side plugins against the reference's UNMODIFIED plugin interface.
 
-integration/xorec_hip_bm.{hpp,cpp} is the class a maintainer adds to the
-reference's src/algorithms/ (INTEGRATION.md §2).  This test compiles it together
+integration/xorec_hip_bm.{hpp,cpp} (one GPU) and xorec_hip_multi_bm.{hpp,cpp}
+(the batch over several GPUs of one process, devices from XEC_DEVICES; no new
+BenchmarkConfig field, bm_config.hpp:25-43) are the classes a maintainer adds
+to the reference's src/algorithms/ (INTEGRATION.md §2, §3).  This test compiles it together
 with the reference's own abstract_bm.cpp and utils.cpp, where they lie under
 /root/reference (abstract_bm.hpp:18-88, abstract_bm.cpp:4-61, utils.cpp:35-127),
 and links it against libxec_hip.so (integration/Makefile; output under a
@@ -41,6 +43,9 @@ def built(tmp_path_factory):
     return out
 
 
+MULTI_OVERRIDES = [o.replace("XorecBenchmarkHip::", "XorecBenchmarkHipMulti::") for o in OVERRIDES]
+
+
 def _nm(path, *flags):
     return subprocess.run(["nm", "-C", *flags, str(path)], capture_output=True, text=True,
                           check=True).stdout
@@ -55,12 +60,36 @@ def test_plugin_overrides_every_virtual(built):
     assert "vtable for XorecBenchmarkHip" in syms
 
 
+def test_multi_plugin_overrides_every_virtual(built):
+    syms = _nm(built / "xorec_hip_multi_bm.o")
+    for name in MULTI_OVERRIDES:
+        assert f" T {name}" in syms, name
+    assert "vtable for XorecBenchmarkHipMulti" in syms
+    # config 5's exchange and the device list (XEC_DEVICES), no config field
+    for name in ("XorecBenchmarkHipMulti::scatter_from(unsigned char const*, int)",
+                 "XorecBenchmarkHipMulti::gather_parity_to(unsigned char*, int)"):
+        assert f" T {name}" in syms, name
+    assert "XEC_DEVICES" in (ROOT / "integration" / "xorec_hip_multi_bm.cpp").read_text()
+
+
+def test_reference_config_is_unmodified():
+    """The plugins use the reference's BenchmarkConfig as it is: every field
+    they read exists in bm_config.hpp:25-43 (no `devices`, no `seed`)."""
+    import re
+    fields = set(re.findall(r"^\s+[\w:<>*]+\s+(\w+)(?:\s*=[^;]*)?;",
+                            (REF / "src/benchmark/bm_config.hpp").read_text(), re.M))
+    for f in ("xorec_hip_bm.cpp", "xorec_hip_multi_bm.cpp", "ref_plugin_main.cpp"):
+        used = set(re.findall(r"(?<![\w])config\.(\w+)", (ROOT / "integration" / f).read_text()))
+        assert used <= fields, (f, used - fields)
+
+
 def test_links_reference_interface_with_libxec(built):
     exe = built / "ref_plugin_main"
     assert exe.exists()
     undef = _nm(exe, "-u")
     # the codec calls go to libxec_hip.so's C ABI, nothing to a CUDA runtime
-    for fn in ("xec_init", "xec_encode", "xec_decode", "xec_erase", "xec_validate_blocks"):
+    for fn in ("xec_init", "xec_encode", "xec_decode", "xec_erase", "xec_validate_blocks",
+               "xec_check_bitmap"):
         assert f" U {fn}" in undef, fn
     assert "cuda" not in undef.lower()
     # the reference's own interface code is what got linked, not this repo's mirror

@@ -109,3 +109,59 @@ class CpuCuda:
 
     def current_stream(self):
         return None
+
+
+def multi_leg_main(argv):
+    """Stand-in for erasure-code-benchmark_amd/bin/xec_multi_leg (bench.py's
+    multi_device leg) with the same options and the same JSON keys, computed on
+    the CPU: shards = the device list's stripe ranges, "scatter" = slice copies
+    from a root batch, per-shard encode, "gather" = the parity slices back,
+    compared with the root's own encode.  Measures nothing."""
+    import argparse
+    import json
+    import sys
+    ap = argparse.ArgumentParser(prog="cpu_rehearsal.py multi-leg")
+    ap.add_argument("--devices", required=True)
+    ap.add_argument("--stripes-per-device", type=int, default=256)
+    ap.add_argument("--data", type=int, default=16)
+    ap.add_argument("--parity", type=int, default=1)
+    ap.add_argument("--block", type=int, default=1 << 20)
+    a = ap.parse_args(argv)
+    devices = [int(x) for x in a.devices.split(",")]
+    k, m, bs, S_per = a.data, a.parity, a.block, a.stripes_per_device
+    S = S_per * len(devices)
+    # keep the rehearsal small whatever shape bench.py passes
+    bs_r = min(bs, 4096)
+    import torch
+    x = CpuXec()
+    root = torch.empty(S * k * bs_r, dtype=torch.uint8)
+    x.fill_splitmix64(root, S, k * bs_r, 1896)
+    ref = torch.empty(S * m * bs_r, dtype=torch.uint8)
+    x.encode(root, ref, S, bs_r, k, m)
+    t0 = time.perf_counter()
+    gathered = torch.empty_like(ref)
+    for i in range(len(devices)):
+        a0, a1 = i * S_per, (i + 1) * S_per
+        shard = root[a0 * k * bs_r:a1 * k * bs_r].clone()  # "scatter"
+        par = torch.empty(S_per * m * bs_r, dtype=torch.uint8)
+        x.encode(shard, par, S_per, bs_r, k, m)
+        gathered[a0 * m * bs_r:a1 * m * bs_r] = par  # "gather"
+    t = time.perf_counter() - t0
+    exact = bool(torch.equal(gathered, ref))
+    out = {"plugin": "CPU REHEARSAL stand-in (tools/cpu_rehearsal.py): not a measurement",
+           "rehearsal": True, "devices": devices, "k": k, "m": m, "block_bytes": bs,
+           "stripes_per_device": S_per, "stripes_total": S,
+           "distinct_devices": len(set(devices)), "encode_ms": round(t * 1e3, 4),
+           "decode_ms": round(t * 1e3, 4), "value_GBps": 0.0, "bit_exact": exact,
+           "scatter": {"root": devices[0], "gathered_parity_bit_exact_vs_root_encode": exact}}
+    print(json.dumps(out))
+    sys.exit(0 if exact else 1)
+
+
+if __name__ == "__main__":
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "erasure-code-benchmark_amd"))
+    if len(sys.argv) < 2 or sys.argv[1] != "multi-leg":
+        sys.exit("usage: cpu_rehearsal.py multi-leg --devices LIST [...]")
+    multi_leg_main(sys.argv[2:])
