@@ -153,6 +153,54 @@ def load_traffic(workload):
     return t.get("encode_hbm_bytes_per_launch"), t
 
 
+def rocprof_avg_ns(traffic_src, kernel_base):
+    """The rocprofv3 --kernel-trace --stats average (AverageNs) of the kernel
+    whose name starts with `kernel_base`, from the kernel-stats CSV that
+    profiles/traffic_<workload>.json names as its timing source -- the same
+    profiling session as its PMC bytes (tools/pmc_traffic.py).  Returns
+    {"avg_ns", "calls", "kernel", "source"} or None (no such file or row)."""
+    import csv
+    src = (traffic_src or {}).get("timing_source")
+    if not src:
+        return None
+    path = ROOT / src
+    if not path.exists():
+        return None
+    for row in csv.DictReader(open(path)):
+        name = row["Name"].split("(")[0].replace("void ", "")
+        if name.split("<")[0] == kernel_base:
+            return {"avg_ns": float(row["AverageNs"]), "calls": int(row["Calls"]),
+                    "kernel": name, "source": src}
+    return None
+
+
+def roofline(kernel, b, ms_hip, hbm, traffic_src):
+    """SURVEY.md §8(d) roofline of one kernel: `achieved` = algorithmic bytes
+    per launch / the kernel's rocprofv3 average duration (AverageNs of the
+    kernel-stats CSV the traffic file names, so the line's frac is
+    recomputable from profiles/), when that profile exists for this kernel and
+    batch; else the HIP-event average of this run.  The HIP-event figures of
+    this run are always beside it (`*_hip_events`)."""
+    hip = b / (ms_hip * 1e-3) / 1e9
+    base = kernel.split("<")[0].split(" ")[0]
+    prof = rocprof_avg_ns(traffic_src, base)
+    achieved = b / prof["avg_ns"] if prof else hip  # bytes per ns = GB/s
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": hbm, "kernel": kernel,
+         "algorithmic_bytes_per_launch": b,
+         "avg_launch_ms": round(prof["avg_ns"] * 1e-6 if prof else ms_hip, 4),
+         "timing_source": (f"rocprofv3 --kernel-trace --stats AverageNs of {prof['kernel']} "
+                           f"({prof['calls']} calls): {prof['source']}") if prof else
+                          "HIP events on the launch stream, this run",
+         "achieved_hip_events": round(hip, 1), "frac_hip_events": round(hip / HBM_PEAK_GBPS, 4),
+         "avg_launch_ms_hip_events": round(ms_hip, 4)}
+    if prof:
+        r["rocprof_over_hip_events_ms"] = round(prof["avg_ns"] * 1e-6 / ms_hip, 4)
+    if traffic_src and hbm is not None:
+        r["traffic_source"] = traffic_src.get("source")
+    return r
+
+
 def _cpu_model():
     model, avx512 = "", False
     try:
@@ -795,22 +843,14 @@ def run_rank(args):
         if traffic_src and traffic_src.get("encode_algorithmic_bytes_per_launch") != b_enc:
             traffic, traffic_src = None, None  # profiled at another batch size (--stripes)
         traffic_dec = traffic_src.get("decode_hbm_bytes_per_launch") if traffic_src else None
-
-        def roofline(kernel, b, ms, hbm):
-            achieved = b / (ms * 1e-3) / 1e9
-            r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": hbm,
-                 "kernel": kernel, "algorithmic_bytes_per_launch": b,
-                 "avg_launch_ms": round(ms, 4)}
-            if traffic_src and hbm is not None:
-                r["traffic_source"] = traffic_src.get("source")
-            return r
-
+        if traffic_src and args.lost != 1:
+            traffic_src, traffic, traffic_dec = None, None, None  # profiled at one erasure
         # the dominant kernel is the one the step spends longer in (decode at the
         # BASELINE shapes: in-place writes); both are reported
-        rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic),
-              "decode": roofline(dec_kernel, b_dec, dec_ms, traffic_dec)}
-        dominant = "decode" if dec_ms >= enc_ms else "encode"
+        rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic, traffic_src),
+              "decode": roofline(dec_kernel, b_dec, dec_ms, traffic_dec, traffic_src)}
+        dominant = ("decode" if rl["decode"]["avg_launch_ms"] >= rl["encode"]["avg_launch_ms"]
+                    else "encode")
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.lost == 1 and not args.rehearse_cpu:
             cpu = cpu_baseline(args.workload, k, m, bs, S_per, args.cpu_seconds)
@@ -840,7 +880,7 @@ def run_rank(args):
                        "decode_api": "xec_decode_device" if args.decode_api == "device"
                        else "xec_decode",
                        "decode_tiling": args.decode_tiling or "automatic"},
-            "roofline": dict(rl[dominant], dominant_by="avg launch time"),
+            "roofline": dict(rl[dominant], dominant_by="avg launch time (avg_launch_ms)"),
             # north star: the device-resident rate at every N also as a fraction of
             # the HBM roofline of the N GPUs together (value / (N x 8 TB/s))
             "value_frac_of_n_gpu_hbm_peak": round(value / (world * HBM_PEAK_GBPS), 4),

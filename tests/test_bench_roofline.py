@@ -1,0 +1,59 @@
+"""bench.py's roofline object is recomputable from profiles/ (VERDICT r3 item 2).
+
+`roofline.achieved` / `frac` = algorithmic bytes per launch / the kernel's
+rocprofv3 AverageNs in the kernel-stats CSV that profiles/traffic_<workload>.json
+names as its `timing_source` (the same profiling session as its PMC bytes);
+the HIP-event figures of the run sit beside it.  CPU only: bench.roofline is
+called with a made-up HIP-event time, and the expected frac is recomputed here
+straight from the cited CSV.
+"""
+from __future__ import annotations
+
+import csv
+import json
+
+import pytest
+
+from conftest import ROOT
+
+import bench
+
+
+def _row(path, base):
+    for r in csv.DictReader(open(ROOT / path)):
+        if r["Name"].split("(")[0].replace("void ", "").split("<")[0] == base:
+            return r
+    raise AssertionError(f"{base} not in {path}")
+
+
+@pytest.mark.parametrize("workload", sorted(bench.WORKLOADS))
+def test_frac_recomputes_from_cited_profile(workload):
+    k, m, bs, S, _ = bench.WORKLOADS[workload]
+    b_enc, b_dec = bench.algorithmic_bytes(S, k, m, bs)
+    _, src = bench.load_traffic(workload)
+    assert src is not None and src["encode_algorithmic_bytes_per_launch"] == b_enc
+    assert (ROOT / src["timing_source"]).exists()
+    # the timing source and the traffic source are one profiling session (one tag)
+    assert src["timing_source"].replace("_kernel_stats.csv", "") in src["source"]
+    dec_base = src["decode_kernel"].split("<")[0]
+    for base, b, hbm in (("xec::encode_kernel", b_enc, src["encode_hbm_bytes_per_launch"]),
+                         (dec_base, b_dec, src["decode_hbm_bytes_per_launch"])):
+        r = bench.roofline(base, b, 1.0, hbm, src)
+        avg_ns = float(_row(src["timing_source"], base)["AverageNs"])
+        assert round(b / avg_ns / 8000.0, 3) == round(r["frac"], 3)
+        assert r["avg_launch_ms"] == round(avg_ns * 1e-6, 4)
+        assert src["timing_source"] in r["timing_source"]
+        # the HIP-event figure of this (made-up) run is kept beside it
+        assert r["avg_launch_ms_hip_events"] == 1.0
+        assert abs(r["frac_hip_events"] - b / 1e-3 / 1e9 / 8000.0) < 1e-4
+        assert r["traffic"] == hbm and r["traffic_source"] == src["source"]
+
+
+def test_frac_falls_back_to_hip_events_without_a_profile():
+    r = bench.roofline("xec::encode_kernel", 8_000_000_000, 1.0, None, None)
+    assert r["timing_source"].startswith("HIP events")
+    assert r["frac"] == r["frac_hip_events"] == 1.0
+    # a profile that lacks the kernel (e.g. a forced decode tiling) also falls back
+    src = json.loads((ROOT / "profiles" / "traffic_cfg3.json").read_text())
+    r = bench.roofline("xec::decode_class_kernel", 8_000_000_000, 1.0, None, src)
+    assert r["timing_source"].startswith("HIP events")

@@ -94,6 +94,9 @@ def main():
     enc = [v for n, v in kernels.items() if n.startswith("xec::encode_kernel")]
     if enc and workload in WORKLOADS:
         traffic = {"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)",
+                   # the same session's kernel trace: bench.py's roofline.achieved /
+                   # frac are algorithmic bytes / its AverageNs (bench.rocprof_avg_ns)
+                   "timing_source": f"profiles/{tag}_kernel_stats.csv",
                    "encode_hbm_bytes_per_launch": enc[0]["hbm_bytes_per_launch"],
                    "encode_algorithmic_bytes_per_launch": enc[0]["algorithmic_bytes_per_launch"]}
         dec = [v for n, v in kernels.items() if n.startswith("xec::decode")]
