@@ -235,13 +235,14 @@ def _host_threads():
     return nproc, omp, quota
 
 
-def cpu_time_port(o, xo, k, m, bs, S, budget_s, threads):
+def cpu_time_port(o, xo, batch, k, m, bs, S, budget_s, threads):
     """The oracle's C restatement of the reference CPU plugin loop
     (XorecBenchmark::encode/decode, xorec_bm.cpp:27-58: OpenMP parallel-for over
     stripes calling xorec_encode / xorec_decode, xorec.cpp:24-111) on one
-    resident host batch, single erasure (7c) mod k per stripe; repeated until
-    `budget_s` of wall time.  Returns (GB/s of algorithmic bytes, reps, seconds)."""
-    data, parity = o.batch(S, k, m, bs, threads=threads)
+    resident host batch (`batch` = (data, parity) from o.batch), single erasure
+    (7c) mod k per stripe; repeated until `budget_s` of wall time.  Returns
+    (GB/s of algorithmic bytes, reps, seconds)."""
+    data, parity = batch
     bm = xo.single_erasure_bitmap(S, k, m)
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
     reps, t_tot = 0, 0.0
@@ -251,72 +252,180 @@ def cpu_time_port(o, xo, k, m, bs, S, budget_s, threads):
         assert o.decode_batch(data, parity, S, bs, k, m, bm, threads) == 0
         t_tot += time.perf_counter() - t0
         reps += 1
-    del data, parity
     return reps * (b_enc + b_dec) / t_tot / 1e9, reps, t_tot
 
 
 CPU_SAMPLE_BYTES = 4 << 30  # ~4 GiB of data per sample: far beyond any host LLC
+CPU_SAMPLES = 3             # timed samples per figure: median, min and max reported
 
 
-def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, sample_bytes=CPU_SAMPLE_BYTES):
-    """BASELINE.md §2 / SURVEY.md §8(d): the CPU XOR-EC path timed on this host's
-    cores on a bounded sample of the same workload, as the build's restatement
-    (oracle/xorec_oracle.c, "kind": "port"; in-container agreement with the
-    reference's own compiled code: profiles/r02_cpu_port_vs_ref.json), at `nproc`
-    threads (the affinity mask, as BASELINE.md §2 asks), at OMP_NUM_THREADS when
-    that differs, and at 1 thread, on the same batch.  `value` / `cores` are the
-    faster of the multi-thread counts (both are in `by_threads`).  Also the other
-    BASELINE shapes (cfg2, cfg3, cfg4) at a third of the budget each, as
-    `by_workload`.  Nothing built from the reference runs here."""
+def parse_cpulist(text):
+    """"0-3,8,10-11" (sysfs cpulist) -> [0, 1, 2, 3, 8, 10, 11]."""
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            lo, _, hi = part.partition("-")
+            out.extend(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def cpu_places(threads, numa_node=None, sysfs="/sys", allowed=None):
+    """The CPUs the CPU baseline's `threads` OpenMP threads are bound to, one
+    each (OMP_PLACES, OMP_PROC_BIND=close): CPUs this process may run on (its
+    affinity mask), those on the GPU's NUMA node first, one CPU per physical
+    core before any SMT sibling; the rest of the mask only if the node has too
+    few.  So the threads neither migrate nor leave the node whose memory they
+    first-touch (the batch is filled in parallel by the same threads)."""
+    allowed = sorted(os.sched_getaffinity(0) if allowed is None else allowed)
+    node = set()
+    if numa_node is not None and numa_node >= 0:
+        try:
+            node = set(parse_cpulist(Path(f"{sysfs}/devices/system/node/node{numa_node}/cpulist")
+                                     .read_text()))
+        except OSError:
+            node = set()
+
+    def primary(c):
+        try:
+            sib = parse_cpulist(Path(f"{sysfs}/devices/system/cpu/cpu{c}/topology/"
+                                     "thread_siblings_list").read_text())
+            return min(sib) == c
+        except (OSError, ValueError):
+            return True
+
+    prim = {c: primary(c) for c in allowed}
+    order = ([c for c in allowed if c in node and prim[c]] +
+             [c for c in allowed if c in node and not prim[c]] +
+             [c for c in allowed if c not in node and prim[c]] +
+             [c for c in allowed if c not in node and not prim[c]])
+    return order[:max(1, threads)]
+
+
+def cpu_measure(spec):
+    """Runs in the CPU baseline's child process (bench.py --cpu-baseline-child,
+    started by cpu_baseline with the OpenMP binding in its environment, so the
+    OpenMP runtime reads it at start-up): CPU_SAMPLES timed samples of each
+    figure on one resident batch per shape.  Only this leg imports oracle/."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import xorec_oracle as xo  # the CPU baseline leg is the only bench use of oracle/
 
     o = xo.COracle()
+    threads, budget, nsamp = spec["threads"], spec["budget_s"], spec.get("samples", CPU_SAMPLES)
+
+    def shape(k, m, bs, S_gpu, budget, single_budget):
+        S = max(1, min(S_gpu, spec.get("sample_bytes", CPU_SAMPLE_BYTES) // (k * bs)))
+        batch = o.batch(S, k, m, bs, threads=threads)  # parallel first touch
+        vals, reps, wall = [], 0, 0.0
+        for _ in range(nsamp):
+            v, r, t = cpu_time_port(o, xo, batch, k, m, bs, S, budget / nsamp, threads)
+            vals.append(v)
+            reps += r
+            wall += t
+        res = {"value": round(statistics.median(vals), 2), "unit": "GB/s", "cores": threads,
+               "kind": "port", "samples": [round(v, 2) for v in vals],
+               "min": round(min(vals), 2), "max": round(max(vals), 2),
+               "sample": f"median of {nsamp} samples, {reps} x (encode+decode) in all, of {S} "
+                         f"stripes k={k}+{m} {bs >> 10} KiB ({S * k * bs >> 20} MiB data), "
+                         f"oracle/xorec_oracle.c (restates xorec.cpp:24-111), OpenMP over "
+                         f"stripes as xorec_bm.cpp:30, {threads} threads, {wall:.1f} s wall"}
+        if single_budget:
+            v1, r1, t1 = cpu_time_port(o, xo, batch, k, m, bs, S, single_budget, 1)
+            res["single_thread"] = {"value": round(v1, 2), "unit": "GB/s",
+                                    "sample": f"{r1} x the same batch on 1 thread, {t1:.1f} s wall"}
+        del batch
+        return res
+
+    k, m, bs, S_gpu = spec["k"], spec["m"], spec["bs"], spec["S_gpu"]
+    out = shape(k, m, bs, S_gpu, budget, min(2.0, budget) if spec.get("single", True) else 0)
+    if spec.get("by_workload"):
+        by = {}
+        for name, (kk, mm, bb, SS, _) in WORKLOADS.items():
+            r = out if name == spec["workload"] else shape(kk, mm, bb, SS, budget / 3, budget / 9)
+            by[name] = {kx: r[kx] for kx in ("value", "cores", "min", "max", "single_thread",
+                                               "sample")}
+        out["by_workload"] = by
+    return out
+
+
+def _cpu_child(spec, env, timeout):
+    import subprocess
+    p = subprocess.run([sys.executable, str(Path(__file__).resolve()), "--cpu-baseline-child",
+                        json.dumps(spec)], capture_output=True, text=True, env=env,
+                       timeout=timeout, cwd=str(ROOT))
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        raise RuntimeError(f"CPU baseline child exit {p.returncode}: {p.stderr[-300:]}")
+    return json.loads(lines[-1])
+
+
+def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, numa_node=None,
+                 sample_bytes=CPU_SAMPLE_BYTES):
+    """BASELINE.md §2 / SURVEY.md §8(d): the CPU XOR-EC path timed on this host's
+    cores on a bounded sample of the same workload, as the build's restatement
+    (oracle/xorec_oracle.c, "kind": "port"; in-container agreement with the
+    reference's own compiled code: profiles/r02_cpu_port_vs_ref.json).
+
+    Threads: the CPUs this process may use -- the smallest of the affinity
+    mask, OMP_NUM_THREADS and the cgroup quota (16 on the GPU box: a 16-CPU
+    quota over a 256-CPU mask) -- each bound to its own physical core on the
+    GPU's NUMA node (cpu_places; OMP_PROC_BIND=close, OMP_PLACES), in a child
+    process so the OpenMP runtime starts with that binding.  `value` is the
+    median of CPU_SAMPLES samples (min / max beside it), plus 1 thread and the
+    other BASELINE shapes (`by_workload`).  The same threads UNBOUND
+    (OMP_PROC_BIND=false: the scheduler free to spread them over the whole
+    mask, both sockets) are timed once more as `unbound_diagnostic` -- the
+    placement rounds 1-3 ran with, whose 318 / 382 / 478 GB/s spread this
+    separates from the codec.  Nothing built from the reference runs here."""
     nproc, omp, quota = _host_threads()
-    counts = [nproc] + ([omp] if omp and omp != nproc else [])
-    model = _cpu_model()[0]
-
-    def sample(k, m, bs, S_gpu):
-        return max(1, min(S_gpu, sample_bytes // (k * bs)))
-
-    def one(k, m, bs, S_gpu, budget, threads):
-        S = sample(k, m, bs, S_gpu)
-        v, reps, t = cpu_time_port(o, xo, k, m, bs, S, budget, threads)
-        return {"value": round(v, 2), "unit": "GB/s", "cores": threads, "kind": "port",
-                "sample": f"{reps} x (encode+decode) of {S} stripes k={k}+{m} "
-                          f"{bs >> 10} KiB ({S * k * bs >> 20} MiB data), oracle/xorec_oracle.c "
-                          f"(restates xorec.cpp:24-111), OpenMP over stripes as "
-                          f"xorec_bm.cpp:30, {threads} threads, {t:.1f} s wall"}
-
-    def single(k, m, bs, S_gpu, budget):
-        S = sample(k, m, bs, S_gpu)
-        v1, reps1, t1 = cpu_time_port(o, xo, k, m, bs, S, min(2.0, budget), 1)
-        return {"value": round(v1, 2), "unit": "GB/s",
-                "sample": f"{reps1} x the same batch on 1 thread, {t1:.1f} s wall"}
-
-    runs = [one(k, m, bs, S_gpu, budget_s if i == 0 else budget_s / 3, c)
-            for i, c in enumerate(counts)]
-    best = max(runs, key=lambda r: r["value"])
-    out = dict(best)
-    out["single_thread"] = single(k, m, bs, S_gpu, budget_s)
-    out["cpu_model"] = model
+    threads = max(1, min(x for x in (nproc, omp, int(quota) if quota else None) if x))
+    cpus = cpu_places(threads, numa_node)
+    spec = {"workload": workload, "k": k, "m": m, "bs": bs, "S_gpu": S_gpu,
+            "budget_s": budget_s, "threads": threads, "sample_bytes": sample_bytes,
+            "samples": CPU_SAMPLES, "by_workload": True}
+    base = {kx: v for kx, v in os.environ.items() if not kx.startswith(("OMP_PLACES",
+                                                                         "OMP_PROC_BIND",
+                                                                         "GOMP_CPU_AFFINITY"))}
+    places = ",".join("{%d}" % c for c in cpus)
+    env_bound = dict(base, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES=places)
+    timeout = 8 * budget_s + 240
+    out = _cpu_child(spec, env_bound, timeout)
+    out["cpu_model"] = _cpu_model()[0]
     out["nproc"] = nproc
     out["omp_num_threads"] = omp
     out["cgroup_cpu_quota"] = quota
-    out["by_threads"] = {str(r["cores"]): r["value"] for r in runs}
-    if len(counts) > 1:
-        out["threads_note"] = (f"nproc ({nproc}, the affinity mask) and OMP_NUM_THREADS ({omp}) "
-                               f"differ: both timed, value at the faster ({best['cores']})"
-                               + (f"; cgroup quota {quota} CPUs" if quota else ""))
-    by = {}
-    for name, (kk, mm, bb, SS, _) in WORKLOADS.items():
-        if name == workload:
-            r = dict(best, single_thread=out["single_thread"])
-        else:
-            r = one(kk, mm, bb, SS, budget_s / 3, best["cores"])
-            r["single_thread"] = single(kk, mm, bb, SS, budget_s / 3)
-        by[name] = {kx: r[kx] for kx in ("value", "cores", "single_thread", "sample")}
-    out["by_workload"] = by
+    out["binding"] = {"OMP_PROC_BIND": "close", "OMP_PLACES": places, "cpus": cpus,
+                      "gpu_numa_node": numa_node,
+                      "note": "one thread per physical core of the GPU's NUMA node, within "
+                              "the affinity mask; threads = min(mask, OMP_NUM_THREADS, cgroup "
+                              "quota)"}
+    try:
+        free = _cpu_child(dict(spec, by_workload=False, single=False, budget_s=budget_s / 3),
+                          dict(base, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="false"),
+                          timeout)
+        out["unbound_diagnostic"] = {
+            kx: free[kx] for kx in ("value", "min", "max", "samples", "cores")}
+        out["unbound_diagnostic"]["note"] = (
+            "the same threads unbound (OMP_PROC_BIND=false, scheduler places them anywhere in "
+            "the mask): the placement of rounds 1-3; bound / unbound = "
+            f"{out['value'] / free['value']:.2f}" if free["value"] else "")
+    except (RuntimeError, OSError, ValueError) as e:  # diagnostic only
+        out["unbound_diagnostic"] = {"error": repr(e)[:200]}
+    # BASELINE.md §2 names `nproc` threads: where the mask is wider than the
+    # CPUs this process may use (256 vs a 16-CPU quota on the GPU box) that
+    # count is timed too, unbound, beside the value
+    out["by_threads"] = {str(threads): out["value"]}
+    if nproc > threads:
+        try:
+            wide = _cpu_child(dict(spec, by_workload=False, single=False, budget_s=budget_s / 3,
+                                   threads=nproc),
+                              dict(base, OMP_NUM_THREADS=str(nproc), OMP_PROC_BIND="false"),
+                              timeout)
+            out["by_threads"][str(nproc)] = wide["value"]
+            out["threads_note"] = (f"value at {threads} threads (min of the affinity mask "
+                                   f"{nproc}, OMP_NUM_THREADS {omp}, cgroup quota {quota}); "
+                                   f"{nproc} threads (nproc) unbound: {wide['value']} GB/s")
+        except (RuntimeError, OSError, ValueError) as e:
+            out["threads_note"] = f"{nproc} threads (nproc) not timed: {repr(e)[:120]}"
     return out
 
 
@@ -609,6 +718,10 @@ def launch_ranks(n, argv, grace_s):
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-baseline-child":
+        # the CPU baseline's child (cpu_baseline): CPU only, no torch, no GPU
+        print(json.dumps(cpu_measure(json.loads(sys.argv[2]))), flush=True)
+        return
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.rank_grace))
@@ -853,7 +966,9 @@ def run_rank(args):
                     else "encode")
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.lost == 1 and not args.rehearse_cpu:
-            cpu = cpu_baseline(args.workload, k, m, bs, S_per, args.cpu_seconds)
+            numa = gpu_numa_node(torch, dev) if devname == "cuda" else {}
+            cpu = cpu_baseline(args.workload, k, m, bs, S_per, args.cpu_seconds,
+                               numa.get("numa_node"))
         metric = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
         out = {
             "metric": metric,

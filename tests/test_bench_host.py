@@ -25,35 +25,60 @@ def test_workloads_match_baseline_configs():
 
 def test_cpu_baseline_shape():
     """The restatement ("port"), never the reference binary; the bench's own
-    workload plus the other BASELINE shapes; 1-thread figure beside."""
-    out = bench.cpu_baseline("cfg2", 8, 1, 1 << 16, 1024, 0.2, sample_bytes=16 << 20)
+    workload plus the other BASELINE shapes; 1-thread figure beside; median of
+    CPU_SAMPLES samples with min / max; threads bound one per core (VERDICT r3
+    item 5) and the same threads unbound as a diagnostic."""
+    import os
+    out = bench.cpu_baseline("cfg2", 8, 1, 1 << 16, 1024, 0.3, 0, sample_bytes=16 << 20)
     assert out["kind"] == "port"
     assert out["unit"] == "GB/s" and out["value"] > 0 and out["cores"] >= 1
     assert out["single_thread"]["value"] > 0
     assert "32 stripes" in out["sample"]  # 16 MiB of k=8 x 64 KiB stripes
+    assert len(out["samples"]) == bench.CPU_SAMPLES
+    assert out["min"] <= out["value"] <= out["max"]
     assert set(out["by_workload"]) == {"cfg2", "cfg3", "cfg4"}
     assert out["by_workload"]["cfg2"]["value"] == out["value"]
     for w in out["by_workload"].values():
-        assert w["value"] > 0 and w["single_thread"]["value"] > 0
-    # BASELINE.md §2: nproc threads (and OMP_NUM_THREADS when different), model named
-    import os
-    assert out["nproc"] == len(os.sched_getaffinity(0))
-    assert str(out["nproc"]) in out["by_threads"]
-    assert out["cores"] in (int(c) for c in out["by_threads"])
-    assert out["value"] == max(out["by_threads"].values())
+        assert w["value"] > 0 and w["single_thread"]["value"] > 0 and w["min"] <= w["max"]
+    nproc = len(os.sched_getaffinity(0))
+    assert out["nproc"] == nproc and out["cores"] <= nproc
+    b = out["binding"]
+    assert b["OMP_PROC_BIND"] == "close" and len(b["cpus"]) == out["cores"]
+    assert b["OMP_PLACES"] == ",".join("{%d}" % c for c in b["cpus"])
+    assert out["unbound_diagnostic"]["value"] > 0
+    assert out["by_threads"][str(out["cores"])] == out["value"]
     assert "cpu_model" in out
 
 
-def test_cpu_baseline_times_both_thread_counts(monkeypatch):
-    """OMP_NUM_THREADS below nproc: both counts timed, the difference noted."""
+def test_cpu_baseline_threads_follow_omp_and_nproc_is_timed(monkeypatch):
+    """OMP_NUM_THREADS below nproc: the value runs at OMP_NUM_THREADS (the CPUs
+    this process may use), nproc threads are timed beside it."""
     import os
     nproc = len(os.sched_getaffinity(0))
     if nproc < 2:
         pytest.skip("needs 2 CPUs")
     monkeypatch.setenv("OMP_NUM_THREADS", "1")
-    out = bench.cpu_baseline("cfg2", 8, 1, 1 << 16, 1024, 0.2, sample_bytes=16 << 20)
-    assert set(out["by_threads"]) == {str(nproc), "1"}
-    assert out["omp_num_threads"] == 1 and "differ" in out["threads_note"]
+    out = bench.cpu_baseline("cfg2", 8, 1, 1 << 16, 1024, 0.2, None, sample_bytes=16 << 20)
+    assert out["cores"] == 1 and out["omp_num_threads"] == 1
+    assert set(out["by_threads"]) == {"1", str(nproc)} and "nproc" in out["threads_note"]
+
+
+def test_cpu_places_prefers_the_gpu_node_and_physical_cores(tmp_path):
+    """cpu_places on a made-up two-node sysfs with SMT siblings (c, c + 8)."""
+    node = tmp_path / "devices/system/node"
+    for n, cpus in ((0, "0-3,8-11"), (1, "4-7,12-15")):
+        (node / f"node{n}").mkdir(parents=True)
+        (node / f"node{n}" / "cpulist").write_text(cpus + "\n")
+    for c in range(16):
+        d = tmp_path / f"devices/system/cpu/cpu{c}/topology"
+        d.mkdir(parents=True)
+        d.joinpath("thread_siblings_list").write_text(f"{c % 8},{c % 8 + 8}\n")
+    allowed = set(range(16))
+    assert bench.cpu_places(3, 1, str(tmp_path), allowed) == [4, 5, 6]
+    assert bench.cpu_places(6, 1, str(tmp_path), allowed) == [4, 5, 6, 7, 12, 13]
+    assert bench.cpu_places(10, 0, str(tmp_path), allowed) == [0, 1, 2, 3, 8, 9, 10, 11, 4, 5]
+    assert bench.cpu_places(2, None, str(tmp_path), {9, 2, 1}) == [1, 2]
+    assert bench.parse_cpulist("0-2,7\n") == [0, 1, 2, 7]
 
 
 def test_erasure_pattern_is_recoverable_and_exact():
