@@ -36,6 +36,11 @@ struct Geo {
   // row order: 0 as laid out; p > 0 interleaves p groups of rows/p rows
   // (consecutive tiles' rows are rows/p apart); -1 bit-reverses the row index
   int perm = 0;
+  // column rotation: row r's chunk c reads column chunk
+  // (c + r*rot) mod tiles_per_row, so the blocks of the rows in flight at
+  // once are read at different offsets -- mixes the address bits of the
+  // concurrently read blocks, where `perm` only changed which rows are in flight
+  uint64_t rot = 0;
 };
 
 __device__ __forceinline__ uint64_t row_of(uint64_t r, const Geo& g) {
@@ -55,7 +60,8 @@ __global__ __launch_bounds__(64) void read_kernel(const uint8_t* __restrict__ ba
   const uint64_t t0 = blockIdx.x;
   if (t0 >= g.total_tiles) return;
   const uint64_t t = g.reverse ? g.total_tiles - 1 - t0 : t0;
-  const uint64_t r = row_of(t / g.tiles_per_row, g), c = t % g.tiles_per_row;
+  const uint64_t r = row_of(t / g.tiles_per_row, g);
+  const uint64_t c = (t % g.tiles_per_row + r * g.rot) % g.tiles_per_row;
   const uint8_t* p = base + r * g.row_stride + (r & 1) * g.alt_offset + c * 1024 + threadIdx.x * 16;
   u32x4 v[NM];
 #pragma unroll
@@ -118,6 +124,7 @@ void launch(const Case& cs, const uint8_t* buf, uint8_t* sink, uint32_t lds, hip
   else if (cs.nm == 16) launch_read<16, false>(cs, buf, sink, lds, s);
   else if (cs.nm == 32 && cs.nt) launch_read<32, true>(cs, buf, sink, lds, s);
   else if (cs.nm == 8 && cs.nt) launch_read<8, true>(cs, buf, sink, lds, s);
+  else if (cs.nm == 4 && cs.nt) launch_read<4, true>(cs, buf, sink, lds, s);
   else std::exit(3);
 }
 
@@ -164,6 +171,21 @@ int main(int argc, char** argv) {
   cases.push_back({"d16p2_same_class_rows_by16", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, 0, 16}});
   cases.push_back({"d16p2_same_class_rows_bitrev", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, 0, -1}});
   cases.push_back({"d16p2_alternating_rows_by4", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, MiB, 4}});
+  // column rotation of the same-class reads (one failed device: the same shard
+  // lost in every stripe), R = rotation in 1 KiB chunks per stripe
+  for (uint64_t R : {1ull, 3ull, 16ull, 64ull, 129ull, 256ull, 512ull})
+    cases.push_back({"d16p2_same_class_rot" + std::to_string(R), 8, true,
+                     {16 * MiB, 2 * MiB, 1024, T8, 1, 0, 0, R}});
+  cases.push_back({"d16p2_alternating_rot64", 8, true, {16 * MiB, 2 * MiB, 1024, T8, 1, MiB, 0, 64}});
+  // 8+2 x 1 MiB single erasure: 4 members 2 MiB apart in 8 MiB stripes
+  const uint64_t T4 = 4 * GiB / (4 * KiB);
+  cases.push_back({"d8p2_4x2MiB_same_class", 4, true, {8 * MiB, 2 * MiB, 1024, T4, 1, 0}});
+  cases.push_back({"d8p2_4x2MiB_alternating", 4, true, {8 * MiB, 2 * MiB, 1024, T4, 1, MiB}});
+  for (uint64_t R : {1ull, 64ull, 129ull, 512ull})
+    cases.push_back({"d8p2_same_class_rot" + std::to_string(R), 4, true,
+                     {8 * MiB, 2 * MiB, 1024, T4, 1, 0, 0, R}});
+  // the encode's geometry rotated: must not lose (config 3)
+  cases.push_back({"cfg3_16x1MiB_rot64", 16, true, {16 * MiB, MiB, 1024, T16, 1, 0, 0, 64}});
 
   // Every byte a case reads must lie inside the buffers: the last tile's last
   // member ends at (rows-1)*row_stride + tiles_per_row*1 KiB + (nm-1)*member_stride.
@@ -205,8 +227,11 @@ int main(int argc, char** argv) {
     json += line;
     first = false;
   };
+  const char* only = std::getenv("READ_PROBE_ONLY");  // substring filter on case names
   for (int round = 0; round < 2; ++round) {  // two interleaved passes
     for (const Case& cs : cases) {
+      if (only && cs.name.find(only) == std::string::npos && cs.name.find("cfg3_16x1MiB") != 0)
+        continue;
       if (end_of(cs) > need || cs.g.total_tiles > 0x7fffffffu) {
         std::fprintf(stderr, "case %s reaches %llu bytes of %llu: not launched\n", cs.name.c_str(),
                      (unsigned long long)end_of(cs), (unsigned long long)need);
@@ -232,6 +257,7 @@ int main(int argc, char** argv) {
     }
     // write-only streams of 1 GiB, 1 / 4 KiB contiguous per workgroup
     for (int per : {1, 4}) {
+      if (only) break;
       for (int occ : occs) {
         const uint32_t lds = lds_for_occupancy(occ);
         const uint64_t tiles = GiB / ((uint64_t)per * KiB);  // tiles * per KiB = 1 GiB <= need

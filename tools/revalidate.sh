@@ -1,6 +1,6 @@
 # Re-validation of the current library: randomised GPU campaigns, a soak and a
-# default bench (the r03zd recipe with a tag and a seed base of its own).
-# Usage (inside gpurun): bash tools/r03_revalidate.sh <tag> <seed-base>
+# default bench (randomised campaigns with a tag and a seed base of their own).
+# Usage (inside gpurun): bash tools/revalidate.sh <tag> <seed-base>
 set -o pipefail
 t=${1:?tag}; s=${2:?seed base}
 o=gpurun_out/$t; mkdir -p $o
