@@ -35,10 +35,12 @@ thread_local int g_threads = 0;
 thread_local int g_occupancy = 0;      // waves per SIMD, 0 = automatic
 thread_local int g_decode_tiling = 0;  // 0 auto, 1 stripe, 2 class, 3 list
 thread_local int g_tiling_used = 0;    // xec_decode_tiling_used: this thread's last xec_decode
+thread_local int g_rotation = 0;       // xec_set_rotation: 0 automatic, -1 none, > 0 tiles
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
 constexpr size_t kAlign = 64;           // XOREC_ALIGNMENT
+constexpr int kMaxRotation = 1 << 20;   // xec_set_rotation's upper bound (tiles)
 
 // LDS to reserve per workgroup so that at most `waves` waves of T-thread
 // workgroups are resident per SIMD: a gfx950 CU has 160 KiB of LDS and 4
@@ -399,8 +401,17 @@ void upload_end(Upload& up, hipStream_t stream, bool launched) {
 // is touched once; xec_kernels.hip kEncodeStoreAux / kDecodeStoreAux), one-wave
 // workgroups with one 1 KiB tile each, one workgroup per tile, residency
 // capped per member count (auto_occupancy).
+// Column rotation of the tile kernels (Geometry::rot): the tiles a stripe's
+// column chunks are shifted by, per stripe.  Automatic = kAutoRotation.
+constexpr uint32_t kAutoRotation = 0;
+uint32_t rotation() {
+  const int r = g_rotation;
+  return r > 0 ? (uint32_t)r : r < 0 ? 0u : kAutoRotation;
+}
+
 xec::LaunchShape launch_shape(size_t bs, int auto_w) {
   xec::LaunchShape ls;
+  ls.rot = rotation();
   const int t = g_threads;
   ls.threads = t == 256 ? 256 : 64;
   const int u = g_unroll;
@@ -863,8 +874,15 @@ xec_status xec_set_validate_kernel(int mode) {
   return XEC_SUCCESS;
 }
 
+xec_status xec_set_rotation(int tiles) {
+  if (tiles < -1 || tiles > kMaxRotation) return XEC_INVALID_SIZE;
+  g_rotation = tiles;
+  return XEC_SUCCESS;
+}
+
 xec_status xec_get_tuning(xec_tuning* out) {
   if (out == nullptr) return XEC_INVALID_ALIGNMENT;
+  out->rotation = g_rotation;
   out->unroll = g_unroll;
   out->max_grid = g_max_grid;
   out->cache_policy = g_nt;
@@ -888,7 +906,8 @@ xec_status xec_set_tuning(const xec_tuning* in) {
           XEC_SUCCESS ||
       xec_set_occupancy(in->waves_per_simd) != XEC_SUCCESS ||
       xec_set_decode_tiling(in->decode_tiling) != XEC_SUCCESS ||
-      xec_set_validate_kernel(in->validate_kernel) != XEC_SUCCESS) {
+      xec_set_validate_kernel(in->validate_kernel) != XEC_SUCCESS ||
+      xec_set_rotation(in->rotation) != XEC_SUCCESS) {
     g_unroll = keep.unroll;
     g_max_grid = keep.max_grid;
     g_nt = keep.cache_policy;
@@ -896,6 +915,7 @@ xec_status xec_set_tuning(const xec_tuning* in) {
     g_occupancy = keep.waves_per_simd;
     g_decode_tiling = keep.decode_tiling;
     xec::g_validate_mode = keep.validate_kernel;
+    g_rotation = keep.rotation;
     return XEC_INVALID_SIZE;
   }
   return XEC_SUCCESS;

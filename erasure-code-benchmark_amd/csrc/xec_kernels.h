@@ -16,6 +16,8 @@ struct Geometry {
   uint64_t tiles_per_block;  // ceil(bs / (16 * threads * unroll))
   uint64_t total_tiles;      // S * m * tiles_per_block
   const int32_t* gate;       // decode only: skip all work if *gate != 0 (nullptr = no gate)
+  uint64_t rot;              // column rotation: stripe c's chunk q covers column chunk
+                             // (q + c*rot) mod tiles_per_block (0 = none; xec_set_rotation)
 };
 
 struct LaunchShape {
@@ -24,6 +26,7 @@ struct LaunchShape {
   uint32_t max_grid;  // 0 = one workgroup per tile, else grid-stride over tiles
   bool nt;            // non-temporal loads/stores
   uint32_t lds_bytes; // LDS reserved per workgroup to cap residency (0 = none)
+  uint32_t rot = 0;   // column rotation in tiles per stripe (Geometry::rot)
 };
 
 inline Geometry make_geometry(uint64_t S, uint64_t bs, uint64_t k, uint64_t m,
@@ -38,6 +41,7 @@ inline Geometry make_geometry(uint64_t S, uint64_t bs, uint64_t k, uint64_t m,
   g.tiles_per_block = (bs + tile_bytes - 1) / tile_bytes;
   g.total_tiles = S * m * g.tiles_per_block;
   g.gate = nullptr;
+  g.rot = g.tiles_per_block > 1 ? ls.rot % g.tiles_per_block : 0;
   return g;
 }
 

@@ -100,6 +100,20 @@ __device__ __forceinline__ TileCoord tile_coord(uint64_t t, const Geometry& g) {
   return tc;
 }
 
+// Column rotation (Geometry::rot, xec_set_rotation): stripe c's chunk q covers
+// column chunk (q + c*rot) mod tiles_per_block.  A bijection on each block's
+// chunks, so every byte is still read and written exactly once; it only moves
+// which columns of concurrently read stripes are in flight together.  With
+// one failed device -- the same shard lost in every stripe -- the stripes in
+// flight read the same columns of blocks a power of two apart, which this HBM
+// serves 10-20 % slower than a mix of offsets (tools/lab/read_probe.hip,
+// profiles/r04b; DESIGN.md §3 *Which block is lost*).
+__device__ __forceinline__ uint64_t rotated(uint64_t chunk, uint64_t c, const Geometry& g) {
+  if (g.rot == 0) return chunk;
+  const uint64_t q = chunk + (c * g.rot) % g.tiles_per_block;
+  return q < g.tiles_per_block ? q : q - g.tiles_per_block;
+}
+
 // XOR-reduce the NM members of one class over this lane's U granules and
 // store the result at dst.  Member r lives at base + r*stride, except member
 // `subst`, whose bytes come from `sub` instead (decode: the class parity).
@@ -176,7 +190,7 @@ __global__ __launch_bounds__(T) void encode_kernel(const uint8_t* __restrict__ d
     const TileCoord tc = tile_coord(t, g);
     const uint8_t* base = data + (tc.c * g.k + tc.j) * g.bs;
     uint8_t* dst = parity + (tc.c * g.m + tc.j) * g.bs;
-    const uint64_t off = (tc.chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+    const uint64_t off = (rotated(tc.chunk, tc.c, g) * (uint64_t)(T * U) + threadIdx.x) * 16;
     xor_members<NM, U, NT, T, kEncodeStoreAux>(base, g.m * g.bs, nullptr, -1, dst, off, g.bs,
                                                (uint32_t)g.nm);
   }
@@ -206,8 +220,8 @@ __global__ __launch_bounds__(T) void decode_kernel(uint8_t* data, const uint8_t*
   const uint64_t stride = g.m * g.bs;
   for (uint64_t t0 = blockIdx.x; t0 < g.total_tiles; t0 += gridDim.x) {
     const uint64_t t = g.total_tiles - 1 - t0;  // from the end of the batch, as encode
-    const uint64_t chunk = t % g.tiles_per_block;
     const uint64_t c = t / g.tiles_per_block;
+    const uint64_t chunk = rotated(t % g.tiles_per_block, c, g);
     const uint64_t rowaddr = reinterpret_cast<uint64_t>(bitmap + c * (g.k + g.m));
     const uint64_t end = rowaddr + g.k;
     uint8_t* sdata = data + c * g.k * g.bs;
@@ -264,7 +278,7 @@ __global__ __launch_bounds__(T) void decode_class_kernel(uint8_t* data,
       if (sbyte(row + (uint64_t)r * g.m) == 0) { lost = r; break; }
     if (lost == nm) continue;
     uint8_t* base = data + (tc.c * g.k + tc.j) * g.bs;
-    const uint64_t off = (tc.chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+    const uint64_t off = (rotated(tc.chunk, tc.c, g) * (uint64_t)(T * U) + threadIdx.x) * 16;
     xor_members<NM, U, NT, T, kDecodeStoreAux>(base, stride, parity + (tc.c * g.m + tc.j) * g.bs,
                                                (int)lost, base + (uint64_t)lost * stride, off,
                                                g.bs, nm);
@@ -289,7 +303,7 @@ __device__ __forceinline__ void rebuild_item(uint8_t* data, const uint8_t* __res
   const uint32_t i = item & 0xFFu;
   const uint32_t j = i % m, r = i / m;  // class and member of the lost block
   uint8_t* base = data + (c * g.k + j) * g.bs;
-  const uint64_t off = (chunk * (uint64_t)(T * U) + threadIdx.x) * 16;
+  const uint64_t off = (rotated(chunk, c, g) * (uint64_t)(T * U) + threadIdx.x) * 16;
   xor_members<NM, U, NT, T, kDecodeStoreAux>(base, stride, parity + (c * g.m + j) * g.bs, (int)r,
                                              base + (uint64_t)r * stride, off, g.bs, nm);
 }

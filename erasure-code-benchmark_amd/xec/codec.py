@@ -136,6 +136,11 @@ def set_decode_tiling(tiling: int = 0) -> Status:
     return Status(lib().xec_set_decode_tiling(tiling))
 
 
+def set_rotation(tiles: int = 0) -> Status:
+    """xec_set_rotation: column rotation of the tile kernels (this thread)."""
+    return Status(lib().xec_set_rotation(tiles))
+
+
 def set_validate_kernel(mode: int = 0) -> Status:
     """xec_set_validate_kernel; 0 = automatic (default), 1 = lane per block,
     2 = wave per block (identical results)."""

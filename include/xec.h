@@ -252,6 +252,14 @@ xec_status xec_set_decode_tiling(int tiling);
  * identical.  XEC_INVALID_SIZE outside 0..2. */
 xec_status xec_set_validate_kernel(int mode);
 
+/* Tuning (per thread, like xec_set_launch): column rotation of the encode and
+ * decode tiles.  Stripe c's 1 KiB column chunk q is processed as chunk
+ * (q + c*tiles) mod (chunks per block): a permutation of each block's chunks,
+ * so results are identical; it changes which columns of the stripes in flight
+ * together are read at once.  0 = automatic (the measured default), -1 = none,
+ * 1..2^20 = that many chunks per stripe.  XEC_INVALID_SIZE outside -1..2^20. */
+xec_status xec_set_rotation(int tiles);
+
 /* The calling thread's overrides above as one value.  A caller that fans its
  * calls out to threads of its own (XorecBenchmarkHipMulti's shard workers)
  * reads them with xec_get_tuning and applies them in each worker with
@@ -264,6 +272,7 @@ typedef struct {
   int waves_per_simd;                                /* xec_set_occupancy */
   int decode_tiling;                                 /* xec_set_decode_tiling */
   int validate_kernel;                               /* xec_set_validate_kernel */
+  int rotation;                                      /* xec_set_rotation */
 } xec_tuning;
 xec_status xec_get_tuning(xec_tuning* out);
 xec_status xec_set_tuning(const xec_tuning* in);

@@ -13,7 +13,12 @@ their addresses differ.  Product xec_decode (automatic tiling), HIP events on
 the launching stream, patterns interleaved over rounds; each pattern's
 rebuild is checked against a fresh fill once.
 
-    python tools/lab/loss_pattern_probe.py [--shapes 16,2,1048576,256 ...] [--out f.json]
+With --rotations R1,R2,... every rotation (xec_set_rotation: -1 none, 0 the
+library's automatic choice, > 0 chunks per stripe) is timed in the same
+interleaved rounds, encode included, and each is checked exact.
+
+    python tools/lab/loss_pattern_probe.py [--shapes 16,2,1048576,256 ...] [--rotations -1,3]
+                                           [--out f.json]
 """
 from __future__ import annotations
 
@@ -53,6 +58,8 @@ def main():
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--seed", type=int, default=1896)
     ap.add_argument("--out", default="")
+    ap.add_argument("--rotations", default="",
+                    help="comma list of xec_set_rotation values to A/B in one process")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -76,12 +83,17 @@ def main():
         h = {n: torch.from_numpy(bm.reshape(-1)).pin_memory() for n, bm in pats.items()}
         dev = {n: t.to("cuda") for n, t in h.items()}
         scratch = torch.empty_like(next(iter(dev.values())))
+        rots = [int(x) for x in args.rotations.split(",")] if args.rotations else [None]
         ok = {}
-        for n in pats:  # erase -> decode -> equal to a fresh fill
-            assert xec.erase(d, p, S, bs, k, m, dev[n], s) == 0
-            assert xec.decode(d, p, S, bs, k, m, h[n], scratch, s) == 0
-            assert xec.fill_splitmix64(fresh, S, k * bs, args.seed, s) == 0
-            ok[n] = bool(torch.equal(d, fresh))
+        for rot in rots:
+            if rot is not None:
+                assert xec.set_rotation(rot) == 0
+            for n in pats:  # erase -> decode -> equal to a fresh fill
+                assert xec.encode(d, p, S, bs, k, m, s) == 0
+                assert xec.erase(d, p, S, bs, k, m, dev[n], s) == 0
+                assert xec.decode(d, p, S, bs, k, m, h[n], scratch, s) == 0
+                assert xec.fill_splitmix64(fresh, S, k * bs, args.seed, s) == 0
+                ok[(rot, n)] = bool(torch.equal(d, fresh))
         del fresh
 
         def run(fn):
@@ -94,20 +106,28 @@ def main():
             torch.cuda.synchronize()
             return [ev[i].elapsed_time(ev[i + 1]) for i in range(args.iters)]
 
-        t = {n: [] for n in pats}
-        t_enc = []
+        t = {(rot, n): [] for rot in rots for n in pats}
+        t_enc = {rot: [] for rot in rots}
         for _ in range(args.rounds):
-            t_enc += run(lambda: xec.encode(d, p, S, bs, k, m, s))
+            for rot in rots:
+                if rot is not None:
+                    assert xec.set_rotation(rot) == 0
+                t_enc[rot] += run(lambda: xec.encode(d, p, S, bs, k, m, s))
+                for n in pats:
+                    t[(rot, n)] += run(lambda n=n: xec.decode(d, p, S, bs, k, m, h[n], scratch, s))
+        xec.set_rotation(0)
+        out = {}
+        for rot in rots:
+            e = statistics.median(t_enc[rot])
+            r = {"encode_ms": round(e, 4), "encode_GBps": round(b_enc / e / 1e6, 1),
+                 "tiling": xec.DECODE_KERNELS.get(xec.decode_tiling_used(), "?")}
             for n in pats:
-                t[n] += run(lambda n=n: xec.decode(d, p, S, bs, k, m, h[n], scratch, s))
-        e = statistics.median(t_enc)
-        r = {"encode_ms": round(e, 4), "encode_GBps": round(b_enc / e / 1e6, 1),
-             "tiling": xec.DECODE_KERNELS.get(xec.decode_tiling_used(), "?")}
-        for n in pats:
-            md = statistics.median(t[n])
-            r[n] = {"ms": round(md, 4), "GBps": round(b_dec / md / 1e6, 1), "exact": ok[n]}
-        res["shapes"][shape] = r
-        print(shape, json.dumps(r), flush=True)
+                md = statistics.median(t[(rot, n)])
+                r[n] = {"ms": round(md, 4), "GBps": round(b_dec / md / 1e6, 1),
+                        "exact": ok[(rot, n)]}
+            out["default" if rot is None else f"rot{rot}"] = r
+            print(shape, "default" if rot is None else f"rot{rot}", json.dumps(r), flush=True)
+        res["shapes"][shape] = out if rots != [None] else out["default"]
         del d, p, scratch
         torch.cuda.empty_cache()
     if args.out:
