@@ -401,12 +401,29 @@ void upload_end(Upload& up, hipStream_t stream, bool launched) {
 // is touched once; xec_kernels.hip kEncodeStoreAux / kDecodeStoreAux), one-wave
 // workgroups with one 1 KiB tile each, one workgroup per tile, residency
 // capped per member count (auto_occupancy).
-// Column rotation of the tile kernels (Geometry::rot): the tiles a stripe's
-// column chunks are shifted by, per stripe.  Automatic = kAutoRotation.
-constexpr uint32_t kAutoRotation = 0;
+// Column rotation of the tile kernels (Geometry::rot): the chunks a stripe's
+// column walk is shifted by, per stripe (xec_set_rotation).  Automatic: none
+// for encode and for decodes the host scan cannot see; decode_rotation below.
 uint32_t rotation() {
   const int r = g_rotation;
-  return r > 0 ? (uint32_t)r : r < 0 ? 0u : kAutoRotation;
+  return r > 0 ? (uint32_t)r : 0u;
+}
+
+// Automatic decode rotation.  When every lost data block of the batch sits in
+// one parity class -- one failed device: the same shard gone from every
+// stripe -- with m >= 2, the stripes in flight read the same columns of k/m
+// blocks m*bs apart, which this HBM serves slowly; an odd rotation puts them
+// on different columns.  Measured in one process (tools/lab/
+// loss_pattern_probe.py --rotations, profiles/r04c, r04d): DECODE_ROT_EVIDENCE.
+// Where the class alternates between stripes (the bench's pattern) or several
+// classes lost blocks, a rotation lost up to 11 %, and encode lost 2-15 %, so
+// neither rotates.
+constexpr uint32_t kSameClassRotation = 3;
+constexpr size_t kRotateMinBlock = 256u << 10;
+uint32_t decode_rotation(const XecScan& scan, size_t m, size_t bs) {
+  const int r = g_rotation;
+  if (r != 0) return r > 0 ? (uint32_t)r : 0u;
+  return m >= 2 && scan.lost_class >= 0 && bs >= kRotateMinBlock ? kSameClassRotation : 0u;
 }
 
 xec::LaunchShape launch_shape(size_t bs, int auto_w) {
@@ -572,7 +589,8 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   const bool cls = use_class_tiles(S, m, scan.lost_data);
   if (listable && (tiling == 3 || sparse || (!cls && small))) {
     // one reduction per tile, as encode: encode's residency table
-    const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+    xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+    ls.rot = decode_rotation(scan, m, bs);
     const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
     if (small) {  // the launch copies the list into its kernel arguments
       upload_end(bmu, stream, false);
@@ -635,8 +653,9 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
     return XEC_DEVICE_ERROR;
   }
   // class tiles: one reduction per tile, so the encode's residency table
-  const xec::LaunchShape ls = launch_shape(
+  xec::LaunchShape ls = launch_shape(
       bs, cls ? auto_occupancy(k / m) : decode_auto_occupancy(k / m, scan.lost_data, S));
+  ls.rot = decode_rotation(scan, m, bs);
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   g_tiling_used = cls && m > 1 ? XEC_TILING_CLASS : XEC_TILING_STRIPE;
   const bool ok = xec::launch_decode(d_data, d_parity, bmu.dev, g, ls,

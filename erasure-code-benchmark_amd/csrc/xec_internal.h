@@ -21,6 +21,8 @@ struct XecScan {
   int needs_recovery = 0;     // require_recovery over the batch (bit 0 of a data byte clear)
   uint64_t lost_data = 0;     // zero data bytes
   uint64_t stripes_lost = 0;  // stripes with at least one zero data byte
+  int64_t lost_class = -1;    // the parity class every lost data block is in, or -1
+                              // (none lost, or several classes): one failed device
 };
 
 // xec_check_bitmap plus the counts above (out may be null) and, when `items`

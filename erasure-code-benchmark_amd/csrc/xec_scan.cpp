@@ -38,6 +38,7 @@ struct Visitor {
   int need = 0;
   uint64_t lost_data = 0;  // zero data bytes seen
   uint64_t stripes_lost = 0;
+  int64_t lost_class = -2;  // -2 none yet, -1 several, else the one class
   size_t last_lost_stripe = ~size_t(0);
   std::vector<uint32_t> mark;  // stripe+1 that last marked each class
   uint32_t* items = nullptr;   // optional work list (xec_scan_bitmap)
@@ -58,6 +59,8 @@ struct Visitor {
     if (i < k) {
       if (lost_data < cap) items[lost_data] = xec_work_item(cur_stripe, i);
       ++lost_data;
+      const int64_t c = static_cast<int64_t>(i % m);
+      lost_class = lost_class == -2 ? c : lost_class == c ? c : -1;
       if (last_lost_stripe != cur_stripe) {
         last_lost_stripe = cur_stripe;
         ++stripes_lost;
@@ -135,7 +138,7 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
   const __m256i one = _mm256_set1_epi8(1), zero = _mm256_setzero_si256();
   const size_t n = S * row;
   alignas(32) uint8_t pad[64];
-  uint64_t need = 0, lost = 0, stripes_lost = 0;
+  uint64_t need = 0, lost = 0, stripes_lost = 0, zd_or = 0;
   for (size_t c = 0; c < S; ++c) {
     const uint8_t* r = bm + c * row;
     if (c * row + 64 > n) {  // last rows: never read past the caller's buffer
@@ -162,6 +165,7 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
     }
     lost += static_cast<uint64_t>(__builtin_popcountll(zd));
     stripes_lost += zd != 0;
+    zd_or |= zd;  // every data position lost anywhere in the batch
     if (z & (z - 1)) {  // two or more zero bytes: they must be in different classes
       if (m == 1) return 0;
       uint64_t seen = 0, bits = z;
@@ -176,6 +180,14 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
   out->needs_recovery = need != 0;
   out->lost_data = lost;
   out->stripes_lost = stripes_lost;
+  // one class iff every position in the union of the losses is in one class
+  out->lost_class = -1;
+  if (zd_or != 0) {
+    const uint8_t c0 = cls[__builtin_ctzll(zd_or)];
+    bool one = true;
+    for (uint64_t b = zd_or; b && one; b &= b - 1) one = cls[__builtin_ctzll(b)] == c0;
+    if (one) out->lost_class = c0;
+  }
   return 1;
 }
 #endif
@@ -317,6 +329,7 @@ xec_status xec_scan_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m, XecS
   r.needs_recovery = v.need;
   r.lost_data = v.lost_data;
   r.stripes_lost = v.stripes_lost;
+  r.lost_class = v.lost_class >= 0 ? v.lost_class : -1;
   if (out) *out = r;
   return XEC_SUCCESS;
 }

@@ -293,6 +293,63 @@ def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
         gpu.set_decode_tiling(0)
 
 
+@pytest.mark.parametrize("rot", [-1, 0, 1, 3, 129, 1 << 20])
+@pytest.mark.parametrize("S,k,m,bs,pattern,tiling", [
+    (16, 16, 2, 1 << 20, "device", 0),   # one failed device at 1 MiB: automatic rotation engages
+    (16, 8, 2, 1 << 20, "device", 1),    # the same on stripe tiles
+    (12, 16, 4, 1 << 20, "device", 2),   # ... class tiles
+    (2048, 4, 1, 256, "device", 3),      # one chunk per block: rotation is the identity
+    (40, 32, 8, 4352, "all", 0),         # ragged tail chunk moved by the rotation
+    (33, 8, 2, 2048 + 768, "one", 3),    # ragged, device-memory list
+    (9, 10, 5, 768, "all", 0),           # generic member count, one ragged chunk
+])
+def test_rotation_bit_exact(gpu, oracle, rot, S, k, m, bs, pattern, tiling):
+    """xec_set_rotation: every column rotation, automatic (0) and none (-1)
+    included, gives the oracle's parity and rebuilds the same bytes, on every
+    decode tiling, ragged tail chunks included (round 4)."""
+    assert gpu.set_rotation(rot) == gpu.Status.SUCCESS
+    assert gpu.set_decode_tiling(tiling) == gpu.Status.SUCCESS
+    try:
+        b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+        bm = np.ones((S, k + m), np.uint8)
+        rng = np.random.default_rng(S * 7 + k)
+        for c in range(S):
+            if pattern == "device":
+                bm[c, k // 3] = 0
+            elif pattern == "one":
+                bm[c, int(rng.integers(k))] = 0
+            else:
+                for j in range(m):
+                    bm[c, j + m * int(rng.integers(k // m))] = 0
+        erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+        # the device-resident decodes under the same rotation
+        torch = _torch()
+        d_bm = torch.from_numpy(np.ascontiguousarray(bm.reshape(-1))).to("cuda")
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        work = torch.empty(gpu.device_list_bytes(S, k, m), dtype=torch.uint8, device="cuda")
+        for call in ("device", "device_list"):
+            assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == gpu.Status.SUCCESS
+            if call == "device":
+                st = gpu.decode_device(b.d, b.p, S, bs, k, m, d_bm, status, b.stream)
+            else:
+                st = gpu.decode_device_list(b.d, b.p, S, bs, k, m, d_bm, work, work.numel(),
+                                            status, b.stream)
+            assert st == gpu.Status.SUCCESS
+            assert int(status.item()) == 0
+            assert np.array_equal(b.data(), ref_d), call
+    finally:
+        gpu.set_decode_tiling(0)
+        gpu.set_rotation(0)
+
+
+def test_rotation_argument_range(gpu):
+    for bad in (-2, (1 << 20) + 1):
+        assert gpu.set_rotation(bad) == gpu.Status.INVALID_SIZE
+    for ok in (-1, 0, 5, 1 << 20):
+        assert gpu.set_rotation(ok) == gpu.Status.SUCCESS
+    assert gpu.set_rotation(0) == gpu.Status.SUCCESS
+
+
 @pytest.mark.parametrize("tiling", [1, 2, 3])
 def test_golden_decode_fixtures_each_tiling(gpu, oracle, known_answers, tiling):
     assert gpu.set_decode_tiling(tiling) == gpu.Status.SUCCESS

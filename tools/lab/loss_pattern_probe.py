@@ -4,6 +4,7 @@
 One lost data block per stripe, three patterns over the same batch:
   same      -- block 0 in every stripe: one failed device (the common case in
                a real system: the same shard index is gone from every stripe)
+  same2     -- blocks 0 and 1 in every stripe (m >= 2): two failed devices
   rotating  -- block (7c) mod k: bench.py's pattern
   random    -- a seeded uniform block per stripe, like the reference's
                select_lost_blocks (src/utils/utils.cpp)
@@ -48,6 +49,11 @@ def patterns(np, S, k, m, seed):
         bm = np.ones((S, k + m), dtype=np.uint8)
         bm[c, idx] = 0
         out[name] = bm
+    if m >= 2:  # two failed devices: blocks 0 and 1 (two classes) gone from every stripe
+        bm = np.ones((S, k + m), dtype=np.uint8)
+        bm[:, 0] = 0
+        bm[:, 1] = 0
+        out["same2"] = bm
     return out
 
 
@@ -78,7 +84,7 @@ def main():
         fresh = torch.empty_like(d)
         assert xec.fill_splitmix64(d, S, k * bs, args.seed, s) == 0
         assert xec.encode(d, p, S, bs, k, m, s) == 0
-        b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
+        b_enc, b_dec1 = algorithmic_bytes(S, k, m, bs)
         pats = patterns(np, S, k, m, args.seed)
         h = {n: torch.from_numpy(bm.reshape(-1)).pin_memory() for n, bm in pats.items()}
         dev = {n: t.to("cuda") for n, t in h.items()}
@@ -123,6 +129,7 @@ def main():
                  "tiling": xec.DECODE_KERNELS.get(xec.decode_tiling_used(), "?")}
             for n in pats:
                 md = statistics.median(t[(rot, n)])
+                b_dec = b_dec1 * (2 if n == "same2" else 1)
                 r[n] = {"ms": round(md, 4), "GBps": round(b_dec / md / 1e6, 1),
                         "exact": ok[(rot, n)]}
             out["default" if rot is None else f"rot{rot}"] = r
