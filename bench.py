@@ -792,6 +792,16 @@ def run_rank(args):
         ranks_seen = dist.get_world_size()
         assert ranks_seen == world, f"process group has {ranks_seen} ranks, expected {world}"
     coll_dev = devname if backend == "nccl" else "cpu"
+    # The multi_device leg's wait: while rank 0's child process measures, the
+    # other ranks wait in a host-side (gloo, TCP) barrier -- an RCCL barrier
+    # would keep a kernel spinning on every GPU the child is timing.  Created
+    # by every rank at start-up (group creation is collective); the leg's
+    # device list is the same on every rank (multi_device_list).
+    side_group = None
+    if use_dist and multi_device_list(args, world, ndev) is not None:
+        import datetime
+        side_group = (dist.new_group(backend="gloo", timeout=datetime.timedelta(
+            seconds=args.multi_timeout + 600)) if backend == "nccl" else dist.group.WORLD)
 
     k, m, bs, S_per, desc = workload_shape(args.workload)
     if args.stripes:
@@ -1148,8 +1158,9 @@ def run_rank(args):
 
     # The multi_device leg (N > 1, or --multi-devices): a child process that
     # opens every device itself, started by rank 0 once all ranks have freed
-    # their buffers and met; the other ranks leave first, so no rank's
-    # collective kernel spins on a GPU while the child measures.
+    # their buffers and met; meanwhile the other ranks wait on the host
+    # (side_group), so no rank's collective kernel spins on a GPU the child is
+    # timing.
     multi = None if bad else multi_device_list(args, world, ndev)
     if multi is not None:
         del sets, scratch, d_bm, d_status, events
@@ -1157,19 +1168,23 @@ def run_rank(args):
             cuda.synchronize()
             torch.cuda.empty_cache()
         if use_dist:
-            dist.barrier()
-            if rank != 0:
-                dist.destroy_process_group()
-                return
-        with markers.region("bench:multi_device"):
-            out["multi_device"] = run_multi_device_leg(args, multi, k, m, bs, S_per)
-        print(json.dumps(out), file=result_out, flush=True)
-        if use_dist:
-            dist.destroy_process_group()
-        return
+            dist.barrier()  # every rank's GPU work is done and its buffers freed
+        if rank == 0:
+            with markers.region("bench:multi_device"):
+                out["multi_device"] = run_multi_device_leg(args, multi, k, m, bs, S_per)
+        if side_group is not None:
+            dist.barrier(group=side_group)  # the others wait here, on the host
     if out is not None:
         print(json.dumps(out), file=result_out, flush=True)
     if use_dist:
+        # The line is out; a teardown that never returns (a peer gone from a
+        # collective) must not hold the run: the process leaves after 120 s.
+        import threading
+        teardown = threading.Timer(120.0, lambda: (print(
+            f"rank {rank}: process-group teardown still running after 120 s; leaving",
+            file=sys.stderr, flush=True), os._exit(1 if bad else 0)))
+        teardown.daemon = True
+        teardown.start()
         # the other ranks wait here while rank 0 writes its line, so nothing they
         # log while tearing down can land inside it when stdout and stderr share
         # one pipe
