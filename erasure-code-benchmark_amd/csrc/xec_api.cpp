@@ -413,13 +413,16 @@ uint32_t rotation() {
 // one parity class -- one failed device: the same shard gone from every
 // stripe -- with m >= 2, the stripes in flight read the same columns of k/m
 // blocks m*bs apart, which this HBM serves slowly; an odd rotation puts them
-// on different columns.  Measured in one process (tools/lab/
-// loss_pattern_probe.py --rotations, profiles/r04c, r04d): DECODE_ROT_EVIDENCE.
-// Where the class alternates between stripes (the bench's pattern) or several
-// classes lost blocks, a rotation lost up to 11 %, and encode lost 2-15 %, so
-// neither rotates.
+// on different columns.  Measured in one process against no rotation
+// (tools/lab/loss_pattern_probe.py --rotations, profiles/r04d): one failed
+// device +15.7 % at 16+2 x 1 MiB, +15.4 % at 8+2, +11.5 % at 16+4, +5.8 % at
+// 32+4, +5.4 % at 16+2 x 512 KiB, +3.8 % at 16+2 x 4 MiB, but -4.0 % at
+// 16+2 x 256 KiB -- hence the 512 KiB floor.  Where the class alternates
+// between stripes (the bench's pattern) or several classes lost blocks, a
+// rotation lost up to 11 %, and encode lost 2-15 % (profiles/r04c), so neither
+// rotates.
 constexpr uint32_t kSameClassRotation = 3;
-constexpr size_t kRotateMinBlock = 256u << 10;
+constexpr size_t kRotateMinBlock = 512u << 10;
 uint32_t decode_rotation(const XecScan& scan, size_t m, size_t bs) {
   const int r = g_rotation;
   if (r != 0) return r > 0 ? (uint32_t)r : 0u;
