@@ -272,7 +272,10 @@ def parse_cpulist(text):
 def cpu_places(threads, numa_node=None, sysfs="/sys", allowed=None):
     """The CPUs the CPU baseline's `threads` OpenMP threads are bound to, one
     each (OMP_PLACES, OMP_PROC_BIND=close): CPUs this process may run on (its
-    affinity mask), those on the GPU's NUMA node first, one CPU per physical
+    affinity mask), those on the GPU's NUMA node first, spread round robin
+    over the node's L3 domains (CCDs on EPYC: each reaches memory through its
+    own link, so 16 threads packed on two CCDs were capped at 132 GB/s where
+    the same threads unbound reached 268, profiles/r04e), one CPU per physical
     core before any SMT sibling; the rest of the mask only if the node has too
     few.  So the threads neither migrate nor leave the node whose memory they
     first-touch (the batch is filled in parallel by the same threads)."""
@@ -285,19 +288,30 @@ def cpu_places(threads, numa_node=None, sysfs="/sys", allowed=None):
         except OSError:
             node = set()
 
-    def primary(c):
+    def first_of(c, rel):
         try:
-            sib = parse_cpulist(Path(f"{sysfs}/devices/system/cpu/cpu{c}/topology/"
-                                     "thread_siblings_list").read_text())
-            return min(sib) == c
+            return min(parse_cpulist(Path(f"{sysfs}/devices/system/cpu/cpu{c}/{rel}")
+                                     .read_text()))
         except (OSError, ValueError):
-            return True
+            return None
 
-    prim = {c: primary(c) for c in allowed}
-    order = ([c for c in allowed if c in node and prim[c]] +
-             [c for c in allowed if c in node and not prim[c]] +
-             [c for c in allowed if c not in node and prim[c]] +
-             [c for c in allowed if c not in node and not prim[c]])
+    prim = {c: first_of(c, "topology/thread_siblings_list") in (c, None) for c in allowed}
+    l3 = {c: first_of(c, "cache/index3/shared_cpu_list") or 0 for c in allowed}
+
+    def spread(cpus):  # round robin over L3 domains, each domain's CPUs in order
+        groups = {}
+        for c in cpus:
+            groups.setdefault(l3[c], []).append(c)
+        lanes = [groups[g] for g in sorted(groups)]
+        out = []
+        for i in range(max((len(x) for x in lanes), default=0)):
+            out += [x[i] for x in lanes if i < len(x)]
+        return out
+
+    order = (spread([c for c in allowed if c in node and prim[c]]) +
+             spread([c for c in allowed if c in node and not prim[c]]) +
+             spread([c for c in allowed if c not in node and prim[c]]) +
+             spread([c for c in allowed if c not in node and not prim[c]]))
     return order[:max(1, threads)]
 
 
@@ -395,9 +409,9 @@ def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, numa_node=None,
     out["cgroup_cpu_quota"] = quota
     out["binding"] = {"OMP_PROC_BIND": "close", "OMP_PLACES": places, "cpus": cpus,
                       "gpu_numa_node": numa_node,
-                      "note": "one thread per physical core of the GPU's NUMA node, within "
-                              "the affinity mask; threads = min(mask, OMP_NUM_THREADS, cgroup "
-                              "quota)"}
+                      "note": "one thread per physical core of the GPU's NUMA node, spread "
+                              "round robin over its L3 domains (CCDs), within the affinity "
+                              "mask; threads = min(mask, OMP_NUM_THREADS, cgroup quota)"}
     try:
         free = _cpu_child(dict(spec, by_workload=False, single=False, budget_s=budget_s / 3),
                           dict(base, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="false"),

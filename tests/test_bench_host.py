@@ -74,11 +74,22 @@ def test_cpu_places_prefers_the_gpu_node_and_physical_cores(tmp_path):
         d.mkdir(parents=True)
         d.joinpath("thread_siblings_list").write_text(f"{c % 8},{c % 8 + 8}\n")
     allowed = set(range(16))
+    # no L3 information: one domain, CPUs in order
     assert bench.cpu_places(3, 1, str(tmp_path), allowed) == [4, 5, 6]
     assert bench.cpu_places(6, 1, str(tmp_path), allowed) == [4, 5, 6, 7, 12, 13]
     assert bench.cpu_places(10, 0, str(tmp_path), allowed) == [0, 1, 2, 3, 8, 9, 10, 11, 4, 5]
     assert bench.cpu_places(2, None, str(tmp_path), {9, 2, 1}) == [1, 2]
     assert bench.parse_cpulist("0-2,7\n") == [0, 1, 2, 7]
+    # two L3 domains per node (cores {0,1}, {2,3} on node 0; {4,5}, {6,7} on node 1):
+    # threads alternate between them before a domain gets its second core
+    for c in range(16):
+        d = tmp_path / f"devices/system/cpu/cpu{c}/cache/index3"
+        d.mkdir(parents=True)
+        base = (c % 8) // 2 * 2
+        d.joinpath("shared_cpu_list").write_text(f"{base},{base + 1},{base + 8},{base + 9}\n")
+    assert bench.cpu_places(4, 0, str(tmp_path), allowed) == [0, 2, 1, 3]
+    assert bench.cpu_places(2, 1, str(tmp_path), allowed) == [4, 6]
+    assert bench.cpu_places(6, 1, str(tmp_path), allowed) == [4, 6, 5, 7, 12, 14]
 
 
 def test_erasure_pattern_is_recoverable_and_exact():
