@@ -36,7 +36,6 @@ thread_local int g_occupancy = 0;      // waves per SIMD, 0 = automatic
 thread_local int g_decode_tiling = 0;  // 0 auto, 1 stripe, 2 class, 3 list
 thread_local int g_tiling_used = 0;    // xec_decode_tiling_used: this thread's last xec_decode
 thread_local int g_rotation = 0;       // xec_set_rotation: 0 automatic, -1 none, > 0 tiles
-thread_local int g_list_order = 0;     // xec_set_list_order: 0 automatic, 1 stripe, 2 classes
 
 constexpr size_t kBlockMultiple = 256;  // XOREC_BLOCK_SIZE_MULTIPLE
 constexpr size_t kMinBlock = 256;       // XOREC_MIN_BLOCK_SIZE
@@ -430,40 +429,6 @@ uint32_t decode_rotation(const XecScan& scan, size_t m, size_t bs) {
   return m >= 2 && scan.lost_class >= 0 && bs >= kRotateMinBlock ? kSameClassRotation : 0u;
 }
 
-// Work-list order.  The host scan lists the lost blocks in stripe order, and
-// with one-wave tiles walked in list order only the 2-3 items the chip holds
-// at once are read together.  At m >= 2 with large blocks, two such items that
-// lost blocks of the same class read the same blocks (j, j+m, ...) of stripes
-// k*bs apart -- the one-failed-device geometry, which this HBM reads slowly --
-// while items of different classes read complementary blocks.  Under the
-// reference's random losses (select_lost_blocks, utils.cpp:100-127) the decode
-// ran exactly halfway between the two (tools/lab/loss_pattern_probe.py,
-// profiles/r04d).  So when the losses span several classes the list is
-// reordered to take the classes in turn (round robin, each class in stripe
-// order): neighbours in the list read different classes wherever the counts
-// allow.  The rebuilt bytes do not depend on the order.
-bool interleave_list(const XecScan& scan, size_t m, size_t bs) {
-  const int o = g_list_order;
-  if (o != 0) return o == 2;
-  return m >= 2 && scan.lost_class < 0 && bs >= kRotateMinBlock;
-}
-
-void interleave_classes(uint32_t* items, uint64_t n, size_t m) {
-  if (n < 2 || m < 2) return;
-  std::vector<uint64_t> start(m + 1, 0), fill(m, 0);
-  for (uint64_t q = 0; q < n; ++q) ++start[(items[q] & 0xFFu) % m + 1];
-  for (size_t j = 0; j < m; ++j) start[j + 1] += start[j];
-  std::vector<uint32_t> by_class(n);
-  for (uint64_t q = 0; q < n; ++q) {
-    const size_t j = (items[q] & 0xFFu) % m;
-    by_class[start[j] + fill[j]++] = items[q];
-  }
-  uint64_t out = 0;
-  for (uint64_t r = 0; out < n; ++r)
-    for (size_t j = 0; j < m; ++j)
-      if (start[j] + r < start[j + 1]) items[out++] = by_class[start[j] + r];
-}
-
 xec::LaunchShape launch_shape(size_t bs, int auto_w) {
   xec::LaunchShape ls;
   ls.rot = rotation();
@@ -635,7 +600,6 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
       uint32_t items[xec::kArgItems];
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, items, xec::kArgItems);
       if (st != XEC_SUCCESS) return st;
-      if (interleave_list(scan, m, bs)) interleave_classes(items, scan.lost_data, m);
       g_tiling_used = XEC_TILING_ARG_LIST;
       return xec::launch_decode(d_data, d_parity, nullptr, g, ls, xec::kDecodeArgListTiles,
                                 stream, scan.lost_data, items) == hipSuccess
@@ -662,7 +626,6 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
         upload_end(bmu, stream, false);
         return st;
       }
-      if (interleave_list(scan, m, bs)) interleave_classes(static_cast<uint32_t*>(sg->host), n, m);
       Upload lu;
       bool ok = true;
       if (side() && upload_begin(sg->host, n * 4, dev, lu)) {
@@ -933,12 +896,6 @@ xec_status xec_set_validate_kernel(int mode) {
   return XEC_SUCCESS;
 }
 
-xec_status xec_set_list_order(int order) {
-  if (order < 0 || order > 2) return XEC_INVALID_SIZE;
-  g_list_order = order;
-  return XEC_SUCCESS;
-}
-
 xec_status xec_set_rotation(int tiles) {
   if (tiles < -1 || tiles > kMaxRotation) return XEC_INVALID_SIZE;
   g_rotation = tiles;
@@ -948,7 +905,6 @@ xec_status xec_set_rotation(int tiles) {
 xec_status xec_get_tuning(xec_tuning* out) {
   if (out == nullptr) return XEC_INVALID_ALIGNMENT;
   out->rotation = g_rotation;
-  out->list_order = g_list_order;
   out->unroll = g_unroll;
   out->max_grid = g_max_grid;
   out->cache_policy = g_nt;
@@ -973,8 +929,7 @@ xec_status xec_set_tuning(const xec_tuning* in) {
       xec_set_occupancy(in->waves_per_simd) != XEC_SUCCESS ||
       xec_set_decode_tiling(in->decode_tiling) != XEC_SUCCESS ||
       xec_set_validate_kernel(in->validate_kernel) != XEC_SUCCESS ||
-      xec_set_rotation(in->rotation) != XEC_SUCCESS ||
-      xec_set_list_order(in->list_order) != XEC_SUCCESS) {
+      xec_set_rotation(in->rotation) != XEC_SUCCESS) {
     g_unroll = keep.unroll;
     g_max_grid = keep.max_grid;
     g_nt = keep.cache_policy;
@@ -983,7 +938,6 @@ xec_status xec_set_tuning(const xec_tuning* in) {
     g_decode_tiling = keep.decode_tiling;
     xec::g_validate_mode = keep.validate_kernel;
     g_rotation = keep.rotation;
-    g_list_order = keep.list_order;
     return XEC_INVALID_SIZE;
   }
   return XEC_SUCCESS;

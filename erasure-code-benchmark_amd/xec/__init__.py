@@ -9,7 +9,7 @@ from .codec import (DECODE_KERNELS, Pipeline, build_info, check_args, check_bitm
                     decode_device, decode_device_list, decode_per_stripe, decode_tiling_used,
                     device_list_bytes, encode, erase,
                     fill_splitmix64, init,
-                    set_decode_tiling, set_launch, set_list_order, set_occupancy, set_rotation,
+                    set_decode_tiling, set_launch, set_occupancy, set_rotation,
                     set_validate_kernel,
                     status_string, validate_blocks, write_validation_pattern)
 from .partition import stripe_range
@@ -19,6 +19,6 @@ __all__ = [
     "build_info", "check_args", "check_bitmap", "decode", "decode_device", "decode_device_list",
     "decode_per_stripe", "decode_tiling_used", "device_list_bytes",
     "encode", "erase", "fill_splitmix64", "init", "set_decode_tiling", "set_launch",
-    "set_list_order", "set_occupancy", "set_rotation", "set_validate_kernel", "status_string", "stripe_range", "validate_blocks",
+    "set_occupancy", "set_rotation", "set_validate_kernel", "status_string", "stripe_range", "validate_blocks",
     "write_validation_pattern",
 ]

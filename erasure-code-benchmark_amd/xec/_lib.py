@@ -28,7 +28,7 @@ EXPORTED = (
     "xec_decode_device", "xec_set_occupancy", "xec_set_decode_tiling",
     "xec_set_validate_kernel", "xec_decode_tiling_used", "xec_decode_per_stripe",
     "xec_decode_device_list", "xec_decode_device_list_bytes", "xec_get_tuning",
-    "xec_set_tuning", "xec_set_rotation", "xec_set_list_order",
+    "xec_set_tuning", "xec_set_rotation",
 )
 
 
@@ -36,8 +36,7 @@ class Tuning(ctypes.Structure):
     """xec_tuning (include/xec.h): the calling thread's overrides."""
     _fields_ = [(n, ctypes.c_int) for n in ("unroll", "max_grid", "cache_policy",
                                             "block_threads", "waves_per_simd",
-                                            "decode_tiling", "validate_kernel", "rotation",
-                                            "list_order")]
+                                            "decode_tiling", "validate_kernel", "rotation")]
 
 
 class XecLibraryError(RuntimeError):
@@ -106,7 +105,6 @@ def lib() -> ctypes.CDLL:
         "xec_decode_device_list": ([vp, vp, sz, sz, sz, sz, vp, vp, sz, vp, vp], st),
         "xec_decode_device_list_bytes": ([sz, sz, sz], sz),
         "xec_set_rotation": ([ctypes.c_int], st),
-        "xec_set_list_order": ([ctypes.c_int], st),
         "xec_get_tuning": ([ctypes.POINTER(Tuning)], st),
         "xec_set_tuning": ([ctypes.POINTER(Tuning)], st),
     }

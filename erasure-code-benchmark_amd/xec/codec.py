@@ -141,12 +141,6 @@ def set_rotation(tiles: int = 0) -> Status:
     return Status(lib().xec_set_rotation(tiles))
 
 
-def set_list_order(order: int = 0) -> Status:
-    """xec_set_list_order: order of xec_decode's work list (this thread);
-    0 automatic, 1 stripe order, 2 classes in turn (identical results)."""
-    return Status(lib().xec_set_list_order(order))
-
-
 def set_validate_kernel(mode: int = 0) -> Status:
     """xec_set_validate_kernel; 0 = automatic (default), 1 = lane per block,
     2 = wave per block (identical results)."""

@@ -260,14 +260,6 @@ xec_status xec_set_validate_kernel(int mode);
  * 1..2^20 = that many chunks per stripe.  XEC_INVALID_SIZE outside -1..2^20. */
 xec_status xec_set_rotation(int tiles);
 
-/* Tuning (per thread): the order of xec_decode's work list (list tiles).
- * 1 = stripe order (the host scan's); 2 = parity classes taken in turn, each
- * in stripe order, so neighbouring list entries rebuild blocks of different
- * classes; 0 = automatic (the measured default: 2 when m >= 2, blocks of
- * 512 KiB or more and the losses span several classes, else 1).  Results are
- * identical.  XEC_INVALID_SIZE outside 0..2. */
-xec_status xec_set_list_order(int order);
-
 /* The calling thread's overrides above as one value.  A caller that fans its
  * calls out to threads of its own (XorecBenchmarkHipMulti's shard workers)
  * reads them with xec_get_tuning and applies them in each worker with
@@ -281,7 +273,6 @@ typedef struct {
   int decode_tiling;                                 /* xec_set_decode_tiling */
   int validate_kernel;                               /* xec_set_validate_kernel */
   int rotation;                                      /* xec_set_rotation */
-  int list_order;                                    /* xec_set_list_order */
 } xec_tuning;
 xec_status xec_get_tuning(xec_tuning* out);
 xec_status xec_set_tuning(const xec_tuning* in);

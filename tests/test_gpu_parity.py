@@ -342,34 +342,6 @@ def test_rotation_bit_exact(gpu, oracle, rot, S, k, m, bs, pattern, tiling):
         gpu.set_rotation(0)
 
 
-@pytest.mark.parametrize("order", [0, 1, 2])
-@pytest.mark.parametrize("S,k,m,bs,lost", [
-    (16, 8, 2, 1 << 20, "one"),      # random classes at 1 MiB: automatic interleave, args list
-    (2048, 8, 2, 256, "one"),        # 2,048 entries: the uploaded list
-    (64, 16, 4, 4096, "select"),     # 1..m losses per stripe, reference draw
-    (40, 12, 4, 1024 + 256, "one"),  # ragged chunks
-])
-def test_list_order_bit_exact(gpu, oracle, order, S, k, m, bs, lost):
-    """xec_set_list_order: the work list in stripe order or with the parity
-    classes taken in turn rebuilds the same bytes (round 4)."""
-    assert gpu.set_list_order(order) == gpu.Status.SUCCESS
-    assert gpu.set_decode_tiling(3) == gpu.Status.SUCCESS
-    try:
-        b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
-        bm = np.ones((S, k + m), np.uint8)
-        rng = np.random.default_rng(S + 11 * k)
-        for c in range(S):
-            if lost == "one":
-                bm[c, int(rng.integers(k))] = 0
-            else:
-                oracle.select_lost_blocks(k, m, 1 + c % m, bm[c], 500 + c)
-        erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
-    finally:
-        gpu.set_decode_tiling(0)
-        gpu.set_list_order(0)
-    assert gpu.set_list_order(3) == gpu.Status.INVALID_SIZE
-
-
 def test_rotation_argument_range(gpu):
     for bad in (-2, (1 << 20) + 1):
         assert gpu.set_rotation(bad) == gpu.Status.INVALID_SIZE

@@ -66,8 +66,6 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--rotations", default="",
                     help="comma list of xec_set_rotation values to A/B in one process")
-    ap.add_argument("--list-orders", default="",
-                    help="comma list of xec_set_list_order values, crossed with --rotations")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -91,29 +89,11 @@ def main():
         h = {n: torch.from_numpy(bm.reshape(-1)).pin_memory() for n, bm in pats.items()}
         dev = {n: t.to("cuda") for n, t in h.items()}
         scratch = torch.empty_like(next(iter(dev.values())))
-        rr = [int(x) for x in args.rotations.split(",")] if args.rotations else [None]
-        lo = [int(x) for x in args.list_orders.split(",")] if args.list_orders else [None]
-        rots = [(r, o) for r in rr for o in lo]
-        if rots == [(None, None)]:
-            rots = [None]
-
-        def apply(v):
-            if v is None:
-                return
-            r, o = v
-            if r is not None:
-                assert xec.set_rotation(r) == 0
-            if o is not None:
-                assert xec.set_list_order(o) == 0
-
-        def label(v):
-            if v is None:
-                return "default"
-            r, o = v
-            return "".join([f"rot{r}" if r is not None else "", f"lo{o}" if o is not None else ""])
+        rots = [int(x) for x in args.rotations.split(",")] if args.rotations else [None]
         ok = {}
         for rot in rots:
-            apply(rot)
+            if rot is not None:
+                assert xec.set_rotation(rot) == 0
             for n in pats:  # erase -> decode -> equal to a fresh fill
                 assert xec.encode(d, p, S, bs, k, m, s) == 0
                 assert xec.erase(d, p, S, bs, k, m, dev[n], s) == 0
@@ -136,12 +116,12 @@ def main():
         t_enc = {rot: [] for rot in rots}
         for _ in range(args.rounds):
             for rot in rots:
-                apply(rot)
+                if rot is not None:
+                    assert xec.set_rotation(rot) == 0
                 t_enc[rot] += run(lambda: xec.encode(d, p, S, bs, k, m, s))
                 for n in pats:
                     t[(rot, n)] += run(lambda n=n: xec.decode(d, p, S, bs, k, m, h[n], scratch, s))
         xec.set_rotation(0)
-        xec.set_list_order(0)
         out = {}
         for rot in rots:
             e = statistics.median(t_enc[rot])
@@ -152,8 +132,8 @@ def main():
                 b_dec = b_dec1 * (2 if n == "same2" else 1)
                 r[n] = {"ms": round(md, 4), "GBps": round(b_dec / md / 1e6, 1),
                         "exact": ok[(rot, n)]}
-            out[label(rot)] = r
-            print(shape, label(rot), json.dumps(r), flush=True)
+            out["default" if rot is None else f"rot{rot}"] = r
+            print(shape, "default" if rot is None else f"rot{rot}", json.dumps(r), flush=True)
         res["shapes"][shape] = out if rots != [None] else out["default"]
         del d, p, scratch
         torch.cuda.empty_cache()
