@@ -424,6 +424,25 @@ def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, numa_node=None,
             f"{out['value'] / free['value']:.2f}" if free["value"] else "")
     except (RuntimeError, OSError, ValueError) as e:  # diagnostic only
         out["unbound_diagnostic"] = {"error": repr(e)[:200]}
+    # The same threads bound one per L3 domain over the WHOLE mask (both
+    # sockets on a two-socket box: twice the memory channels, each thread
+    # first-touching its own socket's memory) -- what 16 threads of this host
+    # can reach, beside the GPU-node figure above
+    wide_cpus = cpu_places(threads, None)
+    if wide_cpus != cpus:
+        try:
+            places_all = ",".join("{%d}" % c for c in wide_cpus)
+            every = _cpu_child(dict(spec, by_workload=False, single=False, budget_s=budget_s / 3),
+                               dict(base, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close",
+                                    OMP_PLACES=places_all), timeout)
+            out["all_nodes_diagnostic"] = {
+                kx: every[kx] for kx in ("value", "min", "max", "samples", "cores")}
+            out["all_nodes_diagnostic"]["OMP_PLACES"] = places_all
+            out["all_nodes_diagnostic"]["note"] = (
+                "the same threads bound one per L3 domain across the whole affinity mask "
+                "(every socket), not only the GPU's NUMA node")
+        except (RuntimeError, OSError, ValueError) as e:  # diagnostic only
+            out["all_nodes_diagnostic"] = {"error": repr(e)[:200]}
     # BASELINE.md §2 names `nproc` threads: where the mask is wider than the
     # CPUs this process may use (256 vs a 16-CPU quota on the GPU box) that
     # count is timed too, unbound, beside the value

@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--rotations", default="",
                     help="comma list of xec_set_rotation values to A/B in one process")
+    ap.add_argument("--tiling", type=int, default=0,
+                    help="xec_set_decode_tiling for every decode (0 = automatic)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -74,6 +76,7 @@ def main():
 
     torch.cuda.set_device(0)
     assert xec.init(0) == 0
+    assert xec.set_decode_tiling(args.tiling) == 0
     s = torch.cuda.current_stream()
     res = {"note": "tools/lab/loss_pattern_probe.py: xec_decode by loss pattern, one lost "
                    "data block per stripe; GB/s of algorithmic bytes", "shapes": {}}
