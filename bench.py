@@ -699,6 +699,28 @@ def run_multi_device_leg(args, devices, k, m, bs, S_per):
     return res
 
 
+def host_side_wait(dist, rank, key, timeout_s):
+    """The other ranks wait for rank 0 on the host, through the process
+    group's own rendezvous store (the TCPStore every rank is already
+    connected to): rank 0 sets `key`, the others block on it.  An RCCL barrier
+    here would keep a collective kernel spinning on every GPU while rank 0's
+    multi_device child times them, and a new gloo group would open fresh
+    connections at the end of the run.  Falls back to dist.barrier() where the
+    store is not reachable."""
+    import datetime
+    try:
+        store = dist.distributed_c10d._get_default_store()
+    except (AttributeError, RuntimeError, ValueError):
+        store = None
+    if store is None:
+        dist.barrier()
+        return
+    if rank == 0:
+        store.set(key, "1")
+    else:
+        store.wait([key], datetime.timedelta(seconds=timeout_s))
+
+
 def launch_ranks(n, argv, grace_s):
     """`bench.py --gpus N` with no launcher around it: start N rank processes of
     this same script (one per GPU, LOCAL_RANK = device), the environment
@@ -825,16 +847,6 @@ def run_rank(args):
         ranks_seen = dist.get_world_size()
         assert ranks_seen == world, f"process group has {ranks_seen} ranks, expected {world}"
     coll_dev = devname if backend == "nccl" else "cpu"
-    # The multi_device leg's wait: while rank 0's child process measures, the
-    # other ranks wait in a host-side (gloo, TCP) barrier -- an RCCL barrier
-    # would keep a kernel spinning on every GPU the child is timing.  Created
-    # by every rank at start-up (group creation is collective); the leg's
-    # device list is the same on every rank (multi_device_list).
-    side_group = None
-    if use_dist and multi_device_list(args, world, ndev) is not None:
-        import datetime
-        side_group = (dist.new_group(backend="gloo", timeout=datetime.timedelta(
-            seconds=args.multi_timeout + 600)) if backend == "nccl" else dist.group.WORLD)
 
     k, m, bs, S_per, desc = workload_shape(args.workload)
     if args.stripes:
@@ -1192,8 +1204,8 @@ def run_rank(args):
     # The multi_device leg (N > 1, or --multi-devices): a child process that
     # opens every device itself, started by rank 0 once all ranks have freed
     # their buffers and met; meanwhile the other ranks wait on the host
-    # (side_group), so no rank's collective kernel spins on a GPU the child is
-    # timing.
+    # (host_side_wait), so no rank's collective kernel spins on a GPU the child
+    # is timing.
     multi = None if bad else multi_device_list(args, world, ndev)
     if multi is not None:
         del sets, scratch, d_bm, d_status, events
@@ -1205,8 +1217,8 @@ def run_rank(args):
         if rank == 0:
             with markers.region("bench:multi_device"):
                 out["multi_device"] = run_multi_device_leg(args, multi, k, m, bs, S_per)
-        if side_group is not None:
-            dist.barrier(group=side_group)  # the others wait here, on the host
+        if use_dist:
+            host_side_wait(dist, rank, "xec_bench_multi_device_done", args.multi_timeout + 600)
     if out is not None:
         print(json.dumps(out), file=result_out, flush=True)
     if use_dist:
