@@ -121,7 +121,7 @@ def _decode_via(gpu, path, b, h_bm, d_bm):
 @pytest.mark.parametrize("case", range(N_PATH_CASES))
 def test_random_shape_every_decode_path(gpu, oracle, case):
     """Every decode entry point and forced tiling on the same random shape and
-    loss pattern, bit-exact against the oracle: the batch paths all-or-nothing
+    loss pattern, under a per-case column rotation, bit-exact against the oracle: the batch paths all-or-nothing
     (xorec_gpu_cmp.cu:75-81), xec_decode_per_stripe stripe by stripe
     (xorec_bm.cpp:43-58); parity never written.  k > 256 (the list's limit):
     the list-only entry points must refuse with InvalidSize and touch nothing."""
@@ -131,7 +131,13 @@ def test_random_shape_every_decode_path(gpu, oracle, case):
     S, k, m, bs = _random_case(rng)
     S = max(S, 3)
     S = min(S, max(1, (24 << 20) // (k * bs)))
-    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs, seed=1300 + case)
+    # every case under a column rotation too (xec_set_rotation), encode included
+    assert gpu.set_rotation([0, -1, 1, 3, 129][case % 5]) == gpu.Status.SUCCESS
+    try:
+        b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs, seed=1300 + case)
+    finally:
+        gpu.set_rotation(0)
+    assert gpu.set_rotation([0, -1, 1, 3, 129][case % 5]) == gpu.Status.SUCCESS
     bm = np.ones((S, k + m), np.uint8)
     for c in range(S):
         oracle.select_lost_blocks(k, m, int(rng.integers(0, m + 1)), bm[c], 31 * case + c)
@@ -170,6 +176,7 @@ def test_random_shape_every_decode_path(gpu, oracle, case):
             assert np.array_equal(got, want), (path, S, k, m, bs)
     finally:
         gpu.set_decode_tiling(0)
+        gpu.set_rotation(0)
 
 
 @pytest.mark.parametrize("S,k,m,bs", [(3, 1000, 1, 256), (2, 512, 2, 512), (3, 264, 8, 256),

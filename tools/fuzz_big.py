@@ -5,8 +5,10 @@ property check of tests/test_gpu_fuzz.py, without the CPU oracle, so batches of
 stripe count; fill; encode, parity checked against a torch XOR of each class;
 then a random loss pattern -- uniform (every stripe loses 1..m data blocks in
 distinct classes), sparse (one stripe in ~9), skewed (a few stripes lose up to
-m, the rest nothing), or with lost parity blocks -- erased and rebuilt through
-every decode entry point and forced tiling.  A recoverable batch must come back
+m, the rest nothing), with lost parity blocks, or one failed device (the same
+data block gone from every stripe: the automatic decode rotation's case) --
+erased and rebuilt through every decode entry point and forced tiling, under a
+per-case column rotation (xec_set_rotation: automatic, none or explicit).  A recoverable batch must come back
 bit-exact with parity untouched; one with an unrecoverable stripe must be left
 as erased (xec_decode_per_stripe: failing stripes only).
 
@@ -38,6 +40,9 @@ def loss_pattern(np, rng, S, k, m, kind):
     """Bitmap (S, k+m) uint8, 0 = lost."""
     bm = np.ones((S, k + m), np.uint8)
     nm = k // m
+    if kind == "device":  # one failed device: the same data block in every stripe
+        bm[:, int(rng.integers(0, k))] = 0
+        return bm
     if kind == "uniform":
         nlost = rng.integers(1, m + 1, size=S)
     elif kind == "sparse":
@@ -96,8 +101,10 @@ def main():
         bs = 256 * int(rng.choice([1, 3, 16, 64, 256, 1024, 4096]))
         target = int(rng.integers(128 << 20, 2 << 30))
         S = max(1, target // (k * bs))
-        kind = ["uniform", "sparse", "skewed", "parity"][case % 4]
+        kind = ["uniform", "sparse", "skewed", "parity", "device"][case % 5]
         unrec = case % 7 == 3  # one unrecoverable stripe
+        rot = int(rng.choice([0, 0, -1, 1, 3, 129]))
+        assert xec.set_rotation(rot) == 0
         d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
         p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
         assert xec.fill_splitmix64(d, S, k * bs, 5000 + case, s) == 0
@@ -164,7 +171,7 @@ def main():
             results[path] = bool(ok and par_ok)
             del erased, erased_p
         row = {"case": case, "k": k, "m": m, "bs": bs, "S": S, "GiB": round(S * k * bs / 2**30, 3),
-               "pattern": kind, "lost_data_blocks": int((bm[:, :k] == 0).sum()),
+               "pattern": kind, "rotation": rot, "lost_data_blocks": int((bm[:, :k] == 0).sum()),
                "recoverable": bool(rec.all()), "encode_ok": enc_ok, "decode_ok": results}
         log.append(row)
         bad = (not enc_ok) or not all(results.values())
