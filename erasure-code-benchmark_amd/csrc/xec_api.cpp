@@ -421,6 +421,22 @@ uint32_t rotation() {
 // between stripes (the bench's pattern) or several classes lost blocks, a
 // rotation lost up to 11 %, and encode lost 2-15 % (profiles/r04c), so neither
 // rotates.
+// The lost_class of a work list (xec_decode_per_stripe lists the rebuilt
+// blocks only; its scan has no class summary of its own).
+XecScan items_scan(const uint32_t* items, uint64_t n, size_t m) {
+  XecScan v;
+  v.lost_data = n;
+  for (uint64_t q = 0; q < n; ++q) {
+    const int64_t c = static_cast<int64_t>((items[q] & 0xFFu) % m);
+    if (q == 0) v.lost_class = c;
+    else if (v.lost_class != c) {
+      v.lost_class = -1;
+      break;
+    }
+  }
+  return v;
+}
+
 constexpr uint32_t kSameClassRotation = 3;
 constexpr size_t kRotateMinBlock = 512u << 10;
 uint32_t decode_rotation(const XecScan& scan, size_t m, size_t bs) {
@@ -697,11 +713,17 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
   const xec_status verdict = failures ? XEC_DECODE_FAILURE : XEC_SUCCESS;
   if (n == 0) return verdict;
   if (capturing(stream)) return XEC_DEVICE_ERROR;  // work to queue: see xec_decode
-  const xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
-  const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+  xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+  xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+  // the rebuilt blocks' classes decide the column rotation, as in xec_decode
+  auto rotate_for = [&](const uint32_t* items, uint64_t count) {
+    ls.rot = decode_rotation(items_scan(items, count, m), m, bs);
+    g = xec::make_geometry(S, bs, k, m, ls);
+  };
   if (n <= xec::kArgItems) {
     uint32_t items[xec::kArgItems];
     (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, xec::kArgItems, &n, &failures);
+    rotate_for(items, n);
     g_tiling_used = XEC_TILING_ARG_LIST;
     return xec::launch_decode(d_data, d_parity, nullptr, g, ls, xec::kDecodeArgListTiles, stream,
                               n, items) == hipSuccess
@@ -721,6 +743,7 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
   if (sg == nullptr) return XEC_DEVICE_ERROR;
   uint32_t* items = static_cast<uint32_t*>(sg->host);
   (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, n, &n, &failures);
+  rotate_for(items, n);
   g_tiling_used = XEC_TILING_LIST;
   Upload lu;
   if (busy == 1 && upload_begin(items, n * 4, dev, lu)) {

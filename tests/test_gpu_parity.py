@@ -327,9 +327,14 @@ def test_rotation_bit_exact(gpu, oracle, rot, S, k, m, bs, pattern, tiling):
         d_bm = torch.from_numpy(np.ascontiguousarray(bm.reshape(-1))).to("cuda")
         status = torch.zeros(1, dtype=torch.int32, device="cuda")
         work = torch.empty(gpu.device_list_bytes(S, k, m), dtype=torch.uint8, device="cuda")
-        for call in ("device", "device_list"):
+        h_bm = torch.from_numpy(np.ascontiguousarray(bm.reshape(-1))).pin_memory()
+        for call in ("per_stripe", "device", "device_list"):
             assert gpu.erase(b.d, b.p, S, bs, k, m, d_bm, b.stream) == gpu.Status.SUCCESS
-            if call == "device":
+            if call == "per_stripe":  # rotation from its own list's classes
+                st = gpu.decode_per_stripe(b.d, b.p, S, bs, k, m, h_bm, torch.empty_like(d_bm),
+                                           None, b.stream)
+                status.zero_()
+            elif call == "device":
                 st = gpu.decode_device(b.d, b.p, S, bs, k, m, d_bm, status, b.stream)
             else:
                 st = gpu.decode_device_list(b.d, b.p, S, bs, k, m, d_bm, work, work.numel(),
