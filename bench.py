@@ -1216,7 +1216,10 @@ def run_rank(args):
             dist.barrier()  # every rank's GPU work is done and its buffers freed
         if rank == 0:
             with markers.region("bench:multi_device"):
-                out["multi_device"] = run_multi_device_leg(args, multi, k, m, bs, S_per)
+                try:
+                    out["multi_device"] = run_multi_device_leg(args, multi, k, m, bs, S_per)
+                except Exception as e:  # noqa: BLE001 - the field, never the line or the wait
+                    out["multi_device"] = {"error": repr(e)[:200], "devices": multi}
         if use_dist:
             host_side_wait(dist, rank, "xec_bench_multi_device_done", args.multi_timeout + 600)
     if out is not None:
