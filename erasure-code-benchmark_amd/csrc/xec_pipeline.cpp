@@ -12,10 +12,12 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -114,6 +116,105 @@ class HostCopier {
   std::thread th_;
 };
 
+// Inputs from PAGEABLE host memory.  A H2D copy from pageable memory is
+// staged by HIP and holds the calling thread until its bytes are out, so the
+// copy engine idles whenever this thread does anything else (the next
+// chunk's scan and launch, the previous chunk's copy-out): pageable decode
+// 48.8 against pinned 55.1 GB/s at config 3, with each of the two inputs
+// costing its share (profiles/r03u, r03w).  So the inputs of the NEXT chunk
+// are copied into a pinned staging buffer by this pool of host threads while
+// the current chunk's DMA runs, and every H2D copy reads pinned memory.
+// Jobs are numbered by staging buffer; a buffer holds one job at a time.
+class HostPool {
+ public:
+  using Piece = HostCopier::Piece;
+  HostPool(int device, unsigned threads, size_t jobs)
+      : device_(device), left_(jobs, 0), failed_(jobs, 0) {
+    for (unsigned t = 0; t < threads; ++t) th_.emplace_back([this] { run(); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();  // the queue is drained first
+  }
+  // Once `after` has passed (null: at once), copy `pieces`, cut into tasks of
+  // at most kTaskBytes so that every thread takes a share.  Job `j` must be
+  // idle (wait(j) returned since its last submit).
+  void submit(size_t j, hipEvent_t after, const std::vector<Piece>& pieces) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      failed_[j] = 0;
+      for (const Piece& pc : pieces)
+        for (size_t o = 0; o < pc.bytes; o += kTaskBytes) {
+          const size_t b = pc.bytes - o < kTaskBytes ? pc.bytes - o : kTaskBytes;
+          q_.push_back(Task{j, after, Piece{pc.dst + o, pc.src + o, b}});
+          ++left_[j];
+        }
+    }
+    cv_.notify_all();
+  }
+  // Job j done; false if its event could not be waited for.
+  bool wait(size_t j) {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return left_[j] == 0; });
+    return failed_[j] == 0;
+  }
+  void drain() {
+    for (size_t j = 0; j < left_.size(); ++j) (void)wait(j);
+  }
+
+ private:
+  static constexpr size_t kTaskBytes = 2u << 20;
+  struct Task {
+    size_t job;
+    hipEvent_t after;
+    Piece pc;
+  };
+  void run() {
+    (void)hipSetDevice(device_);
+    for (;;) {
+      Task t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        t = q_.front();
+        q_.pop_front();
+      }
+      // the staging buffer's previous DMA has read it (returns at once once passed)
+      const bool ok = t.after == nullptr || hipEventSynchronize(t.after) == hipSuccess;
+      if (ok) std::memcpy(t.pc.dst, t.pc.src, t.pc.bytes);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!ok) failed_[t.job] = 1;
+        --left_[t.job];
+      }
+      done_cv_.notify_all();
+    }
+  }
+  int device_;
+  std::vector<size_t> left_;  // tasks outstanding per job
+  std::vector<char> failed_;
+  std::deque<Task> q_;
+  bool stop_ = false;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> th_;
+};
+
+// Host threads that stage pageable inputs; XEC_PIPELINE_COPY_THREADS at
+// xec_pipeline_create overrides (0 = none: HIP stages them, the old path).
+constexpr unsigned kStageThreads = 4;
+unsigned stage_threads() {
+  const char* e = std::getenv("XEC_PIPELINE_COPY_THREADS");
+  if (e == nullptr || *e == '\0') return kStageThreads;
+  const long v = std::strtol(e, nullptr, 10);
+  return v < 0 ? 0u : v > 32 ? 32u : (unsigned)v;
+}
+
 }  // namespace
 
 struct xec_pipeline {
@@ -129,9 +230,26 @@ struct xec_pipeline {
     // after the D2H copies into them
     uint8_t* bounce = nullptr;
     hipEvent_t out_done = nullptr;
+    // staged inputs only: a second stream the H2D copies alternate onto, the
+    // event that frees the slot to it and the one the slot's stream joins
+    hipStream_t aux = nullptr;
+    hipEvent_t free_ev = nullptr, aux_done = nullptr;
   };
   std::vector<Slot> slots;
   HostCopier* copier = nullptr;  // made on the first pageable destination
+  // pageable inputs: two pinned buffers laid out as a slot (data, then
+  // parity), each with the event after the DMA that reads it
+  unsigned stage_threads = 0;
+  // XEC_PIPELINE_STAGE_OPTS (A/B): 'a' alternate H2D streams, 'f' first
+  // chunk direct, 'm' main thread waits for the buffer, 'e' stage encode data
+  bool opt_aux = true, opt_first = true, opt_main = false, opt_encode = false;
+  struct Stage {
+    uint8_t* host = nullptr;
+    hipEvent_t read = nullptr;
+    bool recorded = false;
+  };
+  Stage stage[2];
+  HostPool* pool = nullptr;  // made on the first pageable source
 };
 
 namespace {
@@ -141,12 +259,25 @@ void destroy_slots(xec_pipeline* p) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
   delete p->copier;  // drains its queue: nothing reads a bounce buffer after this
   p->copier = nullptr;
+  delete p->pool;  // likewise for the staging buffers
+  p->pool = nullptr;
+  for (auto& st : p->stage) {
+    (void)hipHostFree(st.host);
+    if (st.read) (void)hipEventDestroy(st.read);
+    st = xec_pipeline::Stage{};
+  }
   for (auto& s : p->slots) {
     (void)hipFree(s.data);
     (void)hipFree(s.parity);
     (void)hipFree(s.bitmap);
     (void)hipHostFree(s.bounce);
     if (s.out_done) (void)hipEventDestroy(s.out_done);
+    if (s.free_ev) (void)hipEventDestroy(s.free_ev);
+    if (s.aux_done) (void)hipEventDestroy(s.aux_done);
+    if (s.aux) {
+      (void)hipStreamSynchronize(s.aux);
+      (void)hipStreamDestroy(s.aux);
+    }
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
   p->slots.clear();
@@ -195,11 +326,53 @@ bool ensure_bounce(xec_pipeline* p) {
   return p->copier != nullptr;
 }
 
+// Staging buffers, their events and the pool, for inputs from pageable
+// memory; false if any of them cannot be had (or staging is off).
+bool ensure_stage(xec_pipeline* p) {
+  if (p->stage_threads == 0) return false;
+  const size_t bytes = p->chunk_stripes * (p->k + p->m) * p->bs;
+  for (auto& st : p->stage) {
+    if (st.host == nullptr &&
+        hipHostMalloc(reinterpret_cast<void**>(&st.host), bytes, hipHostMallocDefault) !=
+            hipSuccess) {
+      st.host = nullptr;
+      return false;
+    }
+    if (st.read == nullptr && hipEventCreateWithFlags(&st.read, hipEventDisableTiming) != hipSuccess) {
+      st.read = nullptr;
+      return false;
+    }
+  }
+  for (auto& s : p->slots) {
+    if (!p->opt_aux) break;
+    if (s.aux == nullptr && hipStreamCreateWithFlags(&s.aux, hipStreamNonBlocking) != hipSuccess) {
+      s.aux = nullptr;
+      return false;
+    }
+    for (hipEvent_t* e : {&s.free_ev, &s.aux_done})
+      if (*e == nullptr && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+        *e = nullptr;
+        return false;
+      }
+  }
+  if (p->pool == nullptr) {
+    try {  // no exception crosses the C ABI (a thread may fail to start)
+      p->pool = new HostPool(p->device, p->stage_threads, 2);
+    } catch (...) {
+      p->pool = nullptr;
+    }
+  }
+  return p->pool != nullptr;
+}
+
 // Every queued copy done, the helper's host copies included.
 xec_status sync_all(xec_pipeline* p) {
   xec_status st = XEC_SUCCESS;
+  if (p->pool) p->pool->drain();  // no staging thread reads the caller's memory after this
   for (auto& s : p->slots)
-    if (hipStreamSynchronize(s.stream) != hipSuccess) st = XEC_DEVICE_ERROR;
+    if (hipStreamSynchronize(s.stream) != hipSuccess ||
+        (s.aux && hipStreamSynchronize(s.aux) != hipSuccess))
+      st = XEC_DEVICE_ERROR;
   if (p->copier && !p->copier->drain()) st = XEC_DEVICE_ERROR;
   return st;
 }
@@ -256,6 +429,95 @@ constexpr size_t kSelectiveCopyBytes = 64u << 10;
 // chunks x 3 streams, tools/pageable_probe.py, profiles/r03q).
 constexpr bool kDeferOutputs = true;
 
+// One H2D copy of a chunk's inputs: `bytes` from host `src` to `off` bytes
+// into the slot's data region (or, `parity`, its parity region).
+struct InRun {
+  bool parity;
+  size_t off;
+  const uint8_t* src;
+  size_t bytes;
+};
+
+// A chunk's inputs, staged or not.  Staged runs (source in pageable memory)
+// are first copied by the pool into staging buffer `chunk_no % 2` at the
+// slot's offsets (`prefetch`, while the previous chunk's DMA runs); `issue`
+// then queues every run on the slot's stream -- staged ones from the staging
+// buffer, the rest straight from the caller's pinned memory -- and marks the
+// buffer read once the stream has passed its copies.
+class Inputs {
+ public:
+  Inputs(xec_pipeline* p, bool stage_data, bool stage_parity)
+      : p_(p), sd_(stage_data), sp_(stage_parity),
+        parity_at_(p->chunk_stripes * p->k * p->bs) {}
+  bool staged() const { return sd_ || sp_; }
+  template <typename Runs>
+  void prefetch(size_t chunk_no, Runs&& runs) {
+    if (!staged()) return;
+    auto& st = p_->stage[chunk_no % 2];
+    std::vector<HostPool::Piece> pieces;
+    runs([&](const InRun& r) {
+      if (r.parity ? sp_ : sd_)
+        pieces.push_back({st.host + (r.parity ? parity_at_ : 0) + r.off, r.src, r.bytes});
+      return true;
+    });
+    hipEvent_t after = st.recorded ? st.read : nullptr;
+    failed_[chunk_no % 2] = false;
+    if (after != nullptr && p_->opt_main) {
+      if (hipEventSynchronize(after) != hipSuccess) {  // issue() then fails
+        pieces.clear();
+        failed_[chunk_no % 2] = true;
+      }
+      after = nullptr;
+    }
+    p_->pool->submit(chunk_no % 2, after, pieces);
+  }
+  // `direct`: this chunk's runs all read the caller's memory on the slot's
+  // stream (HIP stages pageable ones) -- the first chunk of a call, so that
+  // its DMA starts at once while the pool stages the next one.
+  template <typename Runs>
+  bool issue(size_t chunk_no, xec_pipeline::Slot& s, Runs&& runs, bool direct = false) {
+    if (!staged() || direct)
+      return runs([&](const InRun& r) {
+        return hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, r.src, r.bytes,
+                              hipMemcpyHostToDevice, s.stream) == hipSuccess;
+      });
+    auto& st = p_->stage[chunk_no % 2];
+    if (!p_->pool->wait(chunk_no % 2) || failed_[chunk_no % 2]) return false;
+    // the runs alternate between the slot's stream and its aux stream, so one
+    // copy's start-up hides behind the other's transfer; aux first waits until
+    // the slot's stream is done with the slot's previous chunk, and the slot's
+    // stream then waits for aux
+    hipStream_t other = s.aux != nullptr ? s.aux : s.stream;
+    if (other != s.stream && (hipEventRecord(s.free_ev, s.stream) != hipSuccess ||
+                              hipStreamWaitEvent(other, s.free_ev, 0) != hipSuccess))
+      return false;
+    size_t n = 0;
+    bool ok = runs([&](const InRun& r) {
+      const bool from_stage = r.parity ? sp_ : sd_;
+      const uint8_t* src = from_stage ? st.host + (r.parity ? parity_at_ : 0) + r.off : r.src;
+      return hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, src, r.bytes,
+                            hipMemcpyHostToDevice, (n++ % 2) ? other : s.stream) == hipSuccess;
+    });
+    if (other != s.stream)
+      ok = (hipEventRecord(s.aux_done, other) == hipSuccess &&
+            hipStreamWaitEvent(s.stream, s.aux_done, 0) == hipSuccess) && ok;
+    if (ok && hipEventRecord(st.read, s.stream) == hipSuccess) {
+      st.recorded = true;
+      return true;
+    }
+    (void)hipStreamSynchronize(other);  // nothing reads the buffer after this
+    (void)hipStreamSynchronize(s.stream);
+    st.recorded = false;
+    return false;
+  }
+
+ private:
+  xec_pipeline* p_;
+  bool sd_, sp_;
+  size_t parity_at_;
+  bool failed_[2] = {false, false};
+};
+
 }  // namespace
 
 extern "C" {
@@ -273,6 +535,14 @@ static xec_status create_impl(xec_pipeline** out, size_t chunk_stripes, size_t b
   auto* p = new (std::nothrow) xec_pipeline;
   if (!p) return XEC_DEVICE_ERROR;
   p->device = dev;
+  p->stage_threads = stage_threads();
+  if (const char* e = std::getenv("XEC_PIPELINE_STAGE_OPTS")) {
+    const std::string o(e);
+    p->opt_aux = o.find('a') != std::string::npos;
+    p->opt_first = o.find('f') != std::string::npos;
+    p->opt_main = o.find('m') != std::string::npos;
+    p->opt_encode = o.find('e') != std::string::npos;
+  }
   p->chunk_stripes = chunk_stripes;
   p->bs = bs;
   p->k = k;
@@ -311,9 +581,11 @@ static xec_status encode_impl(xec_pipeline* p, const void* h_data, void* h_parit
   // a chunk's parity copy-out is queued after the NEXT chunk's input (see
   // kDeferOutputs); with one slot the next chunk would overwrite it first
   const bool defer = kDeferOutputs && ns > 1;
-  // parity bound for pageable memory leaves through the bounce buffers
+  // parity bound for pageable memory leaves through the bounce buffers, data
+  // from pageable memory comes in through the staging buffers
   const bool bounce = S > 0 && !host_pinned(h_parity);
   if (bounce && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
+  Inputs in(p, p->opt_encode && S > 0 && !host_pinned(h_data) && ensure_stage(p), false);
   auto out = [&](size_t chunk) {
     const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
     const size_t si = chunk % ns;
@@ -329,19 +601,27 @@ static xec_status encode_impl(xec_pipeline* p, const void* h_data, void* h_parit
     p->copier->push(si, s.out_done, {{dst + c0 * m * bs, s.bounce, n * m * bs}});
     return true;
   };
-  size_t chunk = 0;
-  for (size_t c0 = 0; c0 < S; c0 += cs, ++chunk) {
+  auto runs = [&](size_t chunk) {
+    return [&, chunk](auto&& f) {
+      const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
+      return f(InRun{false, 0, src + c0 * k * bs, n * k * bs});
+    };
+  };
+  const size_t chunks = (S + cs - 1) / cs;
+  // the first chunk comes in directly (opt_first) while the pool stages the next
+  const size_t first = in.staged() && p->opt_first ? 1 : 0;
+  if (first < chunks) in.prefetch(first, runs(first));
+  for (size_t chunk = 0; chunk < chunks; ++chunk) {
+    const size_t n = (S - chunk * cs) < cs ? (S - chunk * cs) : cs;
     auto& s = p->slots[chunk % ns];
-    const size_t n = (S - c0) < cs ? (S - c0) : cs;
     // stream order serialises reuse of this slot behind its previous chunk
-    if (hipMemcpyAsync(s.data, src + c0 * k * bs, n * k * bs, hipMemcpyHostToDevice, s.stream) !=
-        hipSuccess)
-      return fail(p, XEC_DEVICE_ERROR);
+    if (!in.issue(chunk, s, runs(chunk), chunk < first)) return fail(p, XEC_DEVICE_ERROR);
+    if (chunk >= first && chunk + 1 < chunks) in.prefetch(chunk + 1, runs(chunk + 1));
     xec_status st = xec_encode(s.data, s.parity, n, bs, k, m, s.stream);
     if (st != XEC_SUCCESS) return fail(p, st);
     if (defer ? (chunk > 0 && !out(chunk - 1)) : !out(chunk)) return fail(p, XEC_DEVICE_ERROR);
   }
-  if (defer && chunk > 0 && !out(chunk - 1)) return fail(p, XEC_DEVICE_ERROR);
+  if (defer && chunks > 0 && !out(chunks - 1)) return fail(p, XEC_DEVICE_ERROR);
   return sync_all(p);
 }
 
@@ -359,15 +639,20 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
   const bool selective = m > 1 && bs >= kSelectiveCopyBytes;
   const size_t ns = p->slots.size();
   const bool defer = kDeferOutputs && ns > 1;  // as in xec_pipeline_encode
-  // Pageable h_data: every copy to or from it holds this thread until done.
-  // The rebuilt blocks then leave through the bounce buffers, and a chunk's
-  // data comes in as ONE copy, lost blocks included (their content is never
-  // read), instead of one copy per run of survivors -- ~20 us of host time
-  // per call, against the 1/k more bytes (profiles/r03v).
+  // Pageable h_data: the rebuilt blocks leave through the bounce buffers.
+  // Pageable inputs come in through the staging buffers; when staging is off
+  // (or cannot be had) every copy from pageable h_data holds this thread until
+  // done, so a chunk's data then comes in as ONE copy, lost blocks included
+  // (their content is never read), instead of one copy per run of survivors
+  // -- ~20 us of host time per call, against the 1/k more bytes (profiles/r03v).
   const bool pageable = !host_pinned(h_data);
+  const bool paged_parity = !host_pinned(h_parity);
   if (pageable && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
-  const bool whole_chunks = pageable && !selective;
-  std::vector<uint8_t> class_lost(m);
+  const bool stage = (pageable || paged_parity) && ensure_stage(p);
+  Inputs in(p, stage && pageable, stage && paged_parity);
+  // (the first chunk of a staged call comes in directly, so whole too)
+  const bool whole_direct = pageable && !selective;
+  const bool whole_chunks = whole_direct && !stage;
   // D2H of the rebuilt blocks of `chunk` (only those: a survivor's bytes are
   // already in the caller's buffer)
   auto out = [&](size_t chunk, size_t slot) {
@@ -398,11 +683,39 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
     }
     return true;
   };
-  // Slots go round the chunks that rebuild something (a chunk without a loss
-  // moves nothing), so consecutive rebuilding chunks never share a slot.
-  size_t chunk = 0, used = 0, pending = 0, pending_slot = 0;
-  bool have_pending = false;
-  for (size_t c0 = 0; c0 < S; c0 += cs, ++chunk) {
+  // H2D: the surviving data blocks a rebuild reads (a lost block's content is
+  // never read) and the parity; D2H: only the rebuilt blocks.  With selective
+  // copies only the classes that lost a data block travel (xorec.cpp:79-108
+  // reads nothing else).
+  auto runs = [&](size_t chunk, bool whole) {
+    return [&, chunk, whole](auto&& f) -> bool {
+      const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
+      if (whole && !f(InRun{false, 0, data + c0 * k * bs, n * k * bs})) return false;
+      std::vector<uint8_t> class_lost(m);
+      for (size_t c = c0; c < c0 + n && !whole; ++c) {
+        const uint8_t* bm = h_bitmap + c * row;
+        const size_t base = c * k * bs, sbase = (c - c0) * k * bs, pbase = (c - c0) * m * bs;
+        for (size_t j = 0; j < m; ++j) class_lost[j] = 0;
+        for (size_t i = 0; i < k; ++i)
+          if (bm[i] == 0) class_lost[i % m] = 1;
+        if (!for_runs(k, [&](size_t i) { return bm[i] != 0 && (!selective || class_lost[i % m]); },
+                      [&](size_t i, size_t j) {
+                        return f(InRun{false, sbase + i * bs, data + base + i * bs, (j - i) * bs});
+                      }) ||
+            (selective && !for_runs(m, [&](size_t j) { return class_lost[j] != 0; },
+                                    [&](size_t i, size_t j) {
+                                      return f(InRun{true, pbase + i * bs, par + c * m * bs + i * bs,
+                                                     (j - i) * bs});
+                                    })))
+          return false;
+      }
+      return selective || f(InRun{true, 0, par + c0 * m * bs, n * m * bs});
+    };
+  };
+  // The chunks that rebuild something (a chunk without a loss moves nothing).
+  // Slots go round them, so consecutive rebuilding chunks never share a slot.
+  std::vector<size_t> work;
+  for (size_t c0 = 0, chunk = 0; c0 < S; c0 += cs, ++chunk) {
     const size_t n = (S - c0) < cs ? (S - c0) : cs;
     bool any_lost = false;
     for (size_t c = c0; c < c0 + n && !any_lost; ++c)
@@ -411,37 +724,22 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
           any_lost = true;
           break;
         }
-    if (!any_lost) continue;  // nothing of this chunk crosses the link
-    const size_t slot = used++ % ns;
+    if (any_lost) work.push_back(chunk);
+  }
+  size_t pending = 0, pending_slot = 0;
+  bool have_pending = false;
+  // the first rebuilding chunk comes in directly (opt_first) while the pool
+  // stages the next
+  const size_t first = in.staged() && p->opt_first ? 1 : 0;
+  if (first < work.size()) in.prefetch(first, runs(work[first], whole_chunks));
+  for (size_t u = 0; u < work.size(); ++u) {
+    const size_t chunk = work[u], c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
+    const size_t slot = u % ns;
     auto& s = p->slots[slot];
-    // H2D: the surviving data blocks a rebuild reads (a lost block's content
-    // is never read) and the parity; D2H: only the rebuilt blocks.  With
-    // selective copies only the classes that lost a data block travel
-    // (xorec.cpp:79-108 reads nothing else).
-    if (whole_chunks && hipMemcpyAsync(s.data, data + c0 * k * bs, n * k * bs,
-                                       hipMemcpyHostToDevice, s.stream) != hipSuccess)
+    const bool direct = u < first;
+    if (!in.issue(u, s, runs(chunk, direct ? whole_direct : whole_chunks), direct))
       return fail(p, XEC_DEVICE_ERROR);
-    for (size_t c = c0; c < c0 + n && !whole_chunks; ++c) {
-      const uint8_t* bm = h_bitmap + c * row;
-      const size_t base = c * k * bs, sbase = (c - c0) * k * bs;
-      for (size_t j = 0; j < m; ++j) class_lost[j] = 0;
-      for (size_t i = 0; i < k; ++i)
-        if (bm[i] == 0) class_lost[i % m] = 1;
-      const auto h2d = [&](uint8_t* d, const uint8_t* h) {
-        return [&, d, h](size_t i, size_t j) {
-          return hipMemcpyAsync(d + i * bs, h + i * bs, (j - i) * bs, hipMemcpyHostToDevice,
-                                s.stream) == hipSuccess;
-        };
-      };
-      if (!for_runs(k, [&](size_t i) { return bm[i] != 0 && (!selective || class_lost[i % m]); },
-                    h2d(s.data + sbase, data + base)) ||
-          (selective && !for_runs(m, [&](size_t j) { return class_lost[j] != 0; },
-                                  h2d(s.parity + (c - c0) * m * bs, par + c * m * bs))))
-        return fail(p, XEC_DEVICE_ERROR);
-    }
-    if (!selective && hipMemcpyAsync(s.parity, par + c0 * m * bs, n * m * bs,
-                                     hipMemcpyHostToDevice, s.stream) != hipSuccess)
-      return fail(p, XEC_DEVICE_ERROR);
+    if (u >= first && u + 1 < work.size()) in.prefetch(u + 1, runs(work[u + 1], whole_chunks));
     st = xec_decode(s.data, s.parity, n, bs, k, m, h_bitmap + c0 * row, s.bitmap, s.stream);
     if (st != XEC_SUCCESS) return fail(p, st);
     if (!defer) {

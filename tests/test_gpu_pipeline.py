@@ -98,3 +98,52 @@ def test_pipeline_decode_skipped_chunks_and_pageable(gpu, oracle, ns, lossy_chun
         assert pl.decode(h_d, h_p, S, h_bm) == gpu.Status.SUCCESS
         got = np.asarray(h_d if not pinned else h_d.numpy()).reshape(-1)
         assert np.array_equal(got, ref_d.reshape(-1))
+
+
+@pytest.mark.parametrize("threads,opts", [("0", None), ("1", None), ("4", None), ("4", ""),
+                                          ("4", "a"), ("4", "f"), ("4", "me"), ("4", "afe")])
+@pytest.mark.parametrize("pin_d,pin_p", [(False, False), (False, True), (True, False)])
+@pytest.mark.parametrize("S,k,m,bs,chunk,ns", [(37, 8, 1, 65536, 8, 3), (24, 16, 4, 65536, 5, 2),
+                                              (30, 12, 4, 4096, 7, 1), (9, 8, 2, 1 << 20, 2, 3)])
+def test_pipeline_staged_pageable_inputs(gpu, oracle, monkeypatch, threads, opts, pin_d, pin_p,
+                                         S, k, m, bs, chunk, ns):
+    """Inputs in pageable memory go through the pinned staging buffers, filled by
+    XEC_PIPELINE_COPY_THREADS host threads one chunk ahead (0 = HIP stages them),
+    under every XEC_PIPELINE_STAGE_OPTS variant (a: copies alternate over two
+    streams, f: first chunk direct, m: the calling thread waits for a buffer,
+    e: encode data staged too; unset = the library default): every mix of
+    pinned and pageable data / parity, selective (m > 1, >= 64 KiB) and
+    whole-run copies, one to three slots, ragged last chunk."""
+    monkeypatch.setenv("XEC_PIPELINE_COPY_THREADS", threads)
+    if opts is None:
+        monkeypatch.delenv("XEC_PIPELINE_STAGE_OPTS", raising=False)
+    else:
+        monkeypatch.setenv("XEC_PIPELINE_STAGE_OPTS", opts)
+    ref_d, ref_p = oracle.batch(S, k, m, bs, seed_base=5100 + S)
+
+    def host(a, pin):
+        if not pin:
+            return np.ascontiguousarray(a.reshape(-1)).copy()
+        t = _pinned(a.size)
+        t.numpy()[:] = a.reshape(-1)
+        return t
+
+    def arr(t):
+        return np.asarray(t if isinstance(t, np.ndarray) else t.numpy())
+
+    h_d = host(ref_d, pin_d)
+    with gpu.Pipeline(chunk, bs, k, m, ns) as pl:
+        out_p = host(np.zeros_like(ref_p), pin_p)
+        assert pl.encode(h_d, out_p, S) == gpu.Status.SUCCESS
+        assert np.array_equal(arr(out_p), ref_p.reshape(-1))
+        bm = np.ones((S, k + m), np.uint8)
+        for c in range(0, S, 3):  # every third stripe, 1..m data blocks
+            oracle.select_lost_blocks(k, m, 1 + c % m, bm[c], 37 * c + 1)
+            bm[c, k:] = 1
+            if not (bm[c, :k] == 0).any():
+                bm[c, c % k] = 0
+        arr(h_d).reshape(S, k, bs)[bm[:, :k] == 0] = 0
+        h_p = host(ref_p, pin_p)
+        assert pl.decode(h_d, h_p, S, host(bm, True)) == gpu.Status.SUCCESS
+        assert np.array_equal(arr(h_d), ref_d.reshape(-1))
+        assert np.array_equal(arr(h_p), ref_p.reshape(-1))  # parity is read only

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -37,6 +38,12 @@ def main():
     ap.add_argument("--kinds", default="pinned,pageable",
                     help="comma list of: pinned, pageable, data_pageable_parity_pinned, "
                          "data_pinned_parity_pageable")
+    ap.add_argument("--copy-threads", default="",
+                    help="comma list of XEC_PIPELINE_COPY_THREADS values to A/B in one "
+                         "process (each pipeline reads it at create; 0 = HIP stages pageable "
+                         "inputs); default: the library's")
+    ap.add_argument("--rounds", type=int, default=1,
+                    help="repeat the kinds x copy-threads sweep, interleaved")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -77,9 +84,18 @@ def main():
     kinds = {"pinned": (True, True), "pageable": (False, False),
              "data_pageable_parity_pinned": (False, True),
              "data_pinned_parity_pageable": (True, False)}
-    for kind, (pin_d, pin_p) in kinds.items():
-        if kind not in args.kinds.split(","):
-            continue
+    threads = args.copy_threads.split(",") if args.copy_threads else [None]
+    sweep = [(kind, th) for _ in range(args.rounds) for kind in kinds
+             if kind in args.kinds.split(",") for th in threads]
+    for kind, th in sweep:
+        pin_d, pin_p = kinds[kind]
+        if th is not None:  # "8" or "8:af" (XEC_PIPELINE_STAGE_OPTS letters)
+            n_th, sep, opts = th.partition(":")
+            os.environ["XEC_PIPELINE_COPY_THREADS"] = n_th
+            if sep:
+                os.environ["XEC_PIPELINE_STAGE_OPTS"] = opts
+            else:
+                os.environ.pop("XEC_PIPELINE_STAGE_OPTS", None)
         h_d = torch.empty(nbytes, dtype=torch.uint8)
         h_p = torch.zeros(S * m * bs, dtype=torch.uint8)
         if pin_d:
@@ -105,8 +121,12 @@ def main():
         r["pipeline_decode_GBps_data"] = round(nbytes / t / 1e9, 2)
         r["decode_bit_exact"] = bool(torch.equal(h_d, ref_d)) and not any(rcs)
         pl.close()
-        out[kind] = r
-        print(kind, r, flush=True)
+        name = kind if th is None else f"{kind}/threads{th}"
+        if args.rounds > 1:
+            out.setdefault(name, []).append(r)
+        else:
+            out[name] = r
+        print(name, r, flush=True)
         del h_d, h_p, hv
     if args.out:
         Path(args.out).write_text(json.dumps(out, indent=1))
