@@ -297,9 +297,12 @@ int xec_decode_tiling_used(void);
  * streams.  Host buffers may be pageable (file or socket buffers) or pinned
  * (hipHostMalloc / hipHostRegister); pinned ones run at the link's rate
  * (config 3: encode 54, decode 55 GB/s of data against 57 raw), pageable ones
- * at 53 / 49.  Results bound for pageable memory go through
+ * at 52 / 52.  Results bound for pageable memory go through
  * pinned bounce buffers the pipeline owns, copied out by a helper thread of
- * its own.  The calls return when the results are in host memory.  A
+ * its own; a decode's pageable inputs are staged through two pinned buffers
+ * of chunk_stripes*(k+m)*bs bytes, filled one chunk ahead by a pool of host
+ * threads (4; XEC_PIPELINE_COPY_THREADS at create, 0 = none: HIP stages
+ * them).  The calls return when the results are in host memory.  A
  * pipeline serves one call at a time: threads that stream concurrently each
  * create their own (the library's other entry points may be called from any
  * thread).  Each call runs on the pipeline's device and leaves the caller's
