@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--variants", default="",
                     help="semicolon list of unroll,block_threads,occupancy launch variants to "
                          "cross with --libs in the same process (0,0,0 = the library's default)")
+    ap.add_argument("--rotations", default="",
+                    help="comma list of xec_set_rotation values to cross with --libs "
+                         "(-1 none, 0 automatic, > 0 KiB per stripe); default: each lib's own")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the identical-results check (diagnostic builds that store elsewhere)")
     ap.add_argument("--out", default="")
@@ -80,6 +83,10 @@ def main():
             for v in args.variants.split(";"):
                 u, t, o = (int(x) for x in v.split(","))
                 libs[f"{n}@u{u}t{t}o{o}"] = (L, (u, t, o))
+            continue
+        if args.rotations:
+            for r in (int(x) for x in args.rotations.split(",")):
+                libs[f"{n}@r{r}"] = (L, ("rot", r))
             continue
         for o in occs:
             libs[n if o is None else f"{n}@o{o}"] = (L, o)
@@ -110,7 +117,9 @@ def main():
     # every build must produce the same parity and the same rebuilt data
     ref = None
     def use(L, o):
-        if isinstance(o, tuple):
+        if isinstance(o, tuple) and o[0] == "rot":
+            assert L.xec_set_rotation(o[1]) == 0
+        elif isinstance(o, tuple):
             assert L.xec_set_launch(o[0], 0, 0, o[1]) == 0
             assert L.xec_set_occupancy(o[2]) == 0
         elif o is not None:
