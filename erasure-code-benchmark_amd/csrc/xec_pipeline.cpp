@@ -242,7 +242,12 @@ struct xec_pipeline {
   unsigned stage_threads = 0;
   // XEC_PIPELINE_STAGE_OPTS (A/B): 'a' alternate H2D streams, 'f' first
   // chunk direct, 'm' main thread waits for the buffer, 'e' stage encode data
-  bool opt_aux = true, opt_first = true, opt_main = false, opt_encode = false;
+  bool opt_aux = true, opt_first = true, opt_main = false, opt_encode = true;
+  // 's' (A/B): each chunk's H2D copies start only after the previous chunk's
+  // are done (one input transfer in flight at a time)
+  bool opt_serial = false;
+  hipEvent_t in_done = nullptr;
+  bool in_recorded = false;
   struct Stage {
     uint8_t* host = nullptr;
     hipEvent_t read = nullptr;
@@ -281,6 +286,8 @@ void destroy_slots(xec_pipeline* p) {
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
   p->slots.clear();
+  if (p->in_done) (void)hipEventDestroy(p->in_done);
+  p->in_done = nullptr;
 }
 
 // Whether the host buffer at q is pinned (page-locked and known to HIP).
@@ -476,6 +483,16 @@ class Inputs {
   // its DMA starts at once while the pool stages the next one.
   template <typename Runs>
   bool issue(size_t chunk_no, xec_pipeline::Slot& s, Runs&& runs, bool direct = false) {
+    if (!p_->opt_serial || p_->in_done == nullptr) return issue_impl(chunk_no, s, runs, direct);
+    if (p_->in_recorded && hipStreamWaitEvent(s.stream, p_->in_done, 0) != hipSuccess) return false;
+    if (!issue_impl(chunk_no, s, runs, direct)) return false;
+    p_->in_recorded = hipEventRecord(p_->in_done, s.stream) == hipSuccess;
+    return p_->in_recorded;
+  }
+
+ private:
+  template <typename Runs>
+  bool issue_impl(size_t chunk_no, xec_pipeline::Slot& s, Runs&& runs, bool direct) {
     if (!staged() || direct)
       return runs([&](const InRun& r) {
         return hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, r.src, r.bytes,
@@ -511,7 +528,6 @@ class Inputs {
     return false;
   }
 
- private:
   xec_pipeline* p_;
   bool sd_, sp_;
   size_t parity_at_;
@@ -542,12 +558,15 @@ static xec_status create_impl(xec_pipeline** out, size_t chunk_stripes, size_t b
     p->opt_first = o.find('f') != std::string::npos;
     p->opt_main = o.find('m') != std::string::npos;
     p->opt_encode = o.find('e') != std::string::npos;
+    p->opt_serial = o.find('s') != std::string::npos;
   }
   p->chunk_stripes = chunk_stripes;
   p->bs = bs;
   p->k = k;
   p->m = m;
   p->slots.resize(static_cast<size_t>(nstreams));
+  if (p->opt_serial && hipEventCreateWithFlags(&p->in_done, hipEventDisableTiming) != hipSuccess)
+    p->in_done = nullptr;
   for (auto& s : p->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&s.data, chunk_stripes * k * bs) != hipSuccess ||

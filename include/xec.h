@@ -299,7 +299,7 @@ int xec_decode_tiling_used(void);
  * (config 3: encode 54, decode 55 GB/s of data against 57 raw), pageable ones
  * at 52 / 52.  Results bound for pageable memory go through
  * pinned bounce buffers the pipeline owns, copied out by a helper thread of
- * its own; a decode's pageable inputs are staged through two pinned buffers
+ * its own; pageable inputs are staged through two pinned buffers
  * of chunk_stripes*(k+m)*bs bytes, filled one chunk ahead by a pool of host
  * threads (4; XEC_PIPELINE_COPY_THREADS at create, 0 = none: HIP stages
  * them).  The calls return when the results are in host memory.  A
