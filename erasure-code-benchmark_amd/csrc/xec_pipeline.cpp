@@ -243,9 +243,14 @@ struct xec_pipeline {
   // XEC_PIPELINE_STAGE_OPTS (A/B): 'a' alternate H2D streams, 'f' first
   // chunk direct, 'm' main thread waits for the buffer, 'e' stage encode data
   bool opt_aux = true, opt_first = true, opt_main = false, opt_encode = true;
-  // 's' (A/B): each chunk's H2D copies start only after the previous chunk's
-  // are done (one input transfer in flight at a time)
-  bool opt_serial = false;
+  // Serial inputs: each chunk's H2D copies start only after the previous
+  // chunk's are done (one input transfer in flight at a time).  Measured
+  // (tools/pageable_probe.py, profiles/r04m/staging_default.json, 3 rounds):
+  // encode from pinned data +2 % (53.2 -> 54.3 GB/s; +3.8 % with pageable
+  // parity out), but decode -6 % and encode from pageable data -3 %, so by
+  // default only the encode from pinned data runs serial.  's' / 'n' in
+  // XEC_PIPELINE_STAGE_OPTS force it on / off everywhere (A/B).
+  int opt_serial = -1;  // -1 automatic, 0 never, 1 always
   hipEvent_t in_done = nullptr;
   bool in_recorded = false;
   struct Stage {
@@ -453,9 +458,14 @@ struct InRun {
 // buffer read once the stream has passed its copies.
 class Inputs {
  public:
-  Inputs(xec_pipeline* p, bool stage_data, bool stage_parity)
+  // `serial_auto`: whether the caller's inputs run serial when the pipeline's
+  // option is automatic
+  Inputs(xec_pipeline* p, bool stage_data, bool stage_parity, bool serial_auto = false)
       : p_(p), sd_(stage_data), sp_(stage_parity),
-        parity_at_(p->chunk_stripes * p->k * p->bs) {}
+        serial_(p->opt_serial < 0 ? serial_auto : p->opt_serial == 1),
+        parity_at_(p->chunk_stripes * p->k * p->bs) {
+    p->in_recorded = false;  // a new call: nothing of its own to wait for yet
+  }
   bool staged() const { return sd_ || sp_; }
   template <typename Runs>
   void prefetch(size_t chunk_no, Runs&& runs) {
@@ -483,7 +493,7 @@ class Inputs {
   // its DMA starts at once while the pool stages the next one.
   template <typename Runs>
   bool issue(size_t chunk_no, xec_pipeline::Slot& s, Runs&& runs, bool direct = false) {
-    if (!p_->opt_serial || p_->in_done == nullptr) return issue_impl(chunk_no, s, runs, direct);
+    if (!serial_ || p_->in_done == nullptr) return issue_impl(chunk_no, s, runs, direct);
     if (p_->in_recorded && hipStreamWaitEvent(s.stream, p_->in_done, 0) != hipSuccess) return false;
     if (!issue_impl(chunk_no, s, runs, direct)) return false;
     p_->in_recorded = hipEventRecord(p_->in_done, s.stream) == hipSuccess;
@@ -529,7 +539,7 @@ class Inputs {
   }
 
   xec_pipeline* p_;
-  bool sd_, sp_;
+  bool sd_, sp_, serial_;
   size_t parity_at_;
   bool failed_[2] = {false, false};
 };
@@ -558,15 +568,15 @@ static xec_status create_impl(xec_pipeline** out, size_t chunk_stripes, size_t b
     p->opt_first = o.find('f') != std::string::npos;
     p->opt_main = o.find('m') != std::string::npos;
     p->opt_encode = o.find('e') != std::string::npos;
-    p->opt_serial = o.find('s') != std::string::npos;
+    p->opt_serial = o.find('s') != std::string::npos ? 1 : o.find('n') != std::string::npos ? 0 : -1;
   }
   p->chunk_stripes = chunk_stripes;
   p->bs = bs;
   p->k = k;
   p->m = m;
   p->slots.resize(static_cast<size_t>(nstreams));
-  if (p->opt_serial && hipEventCreateWithFlags(&p->in_done, hipEventDisableTiming) != hipSuccess)
-    p->in_done = nullptr;
+  if (p->opt_serial != 0 && hipEventCreateWithFlags(&p->in_done, hipEventDisableTiming) != hipSuccess)
+    p->in_done = nullptr;  // then inputs are never serialised
   for (auto& s : p->slots) {
     if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&s.data, chunk_stripes * k * bs) != hipSuccess ||
@@ -604,7 +614,8 @@ static xec_status encode_impl(xec_pipeline* p, const void* h_data, void* h_parit
   // from pageable memory comes in through the staging buffers
   const bool bounce = S > 0 && !host_pinned(h_parity);
   if (bounce && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
-  Inputs in(p, p->opt_encode && S > 0 && !host_pinned(h_data) && ensure_stage(p), false);
+  const bool data_pinned = S == 0 || host_pinned(h_data);
+  Inputs in(p, p->opt_encode && !data_pinned && ensure_stage(p), false, data_pinned);
   auto out = [&](size_t chunk) {
     const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
     const size_t si = chunk % ns;

@@ -296,8 +296,8 @@ int xec_decode_tiling_used(void);
  * them chunk by chunk: H2D -> kernel -> D2H, chunks overlapping across
  * streams.  Host buffers may be pageable (file or socket buffers) or pinned
  * (hipHostMalloc / hipHostRegister); pinned ones run at the link's rate
- * (config 3: encode 54, decode 55 GB/s of data against 57 raw), pageable ones
- * at 52 / 52.  Results bound for pageable memory go through
+ * (config 3: encode 55, decode 55 GB/s of data against 57 raw), pageable ones
+ * at 55 / 52.  Results bound for pageable memory go through
  * pinned bounce buffers the pipeline owns, copied out by a helper thread of
  * its own; pageable inputs are staged through two pinned buffers
  * of chunk_stripes*(k+m)*bs bytes, filled one chunk ahead by a pool of host
