@@ -258,7 +258,9 @@ struct xec_pipeline {
     hipEvent_t read = nullptr;
     bool recorded = false;
   };
-  Stage stage[2];
+  static constexpr size_t kMaxStage = 4;
+  Stage stage[kMaxStage];
+  size_t stage_buffers = 2;  // in use (opts digit 2..4, A/B)
   HostPool* pool = nullptr;  // made on the first pageable source
 };
 
@@ -343,7 +345,8 @@ bool ensure_bounce(xec_pipeline* p) {
 bool ensure_stage(xec_pipeline* p) {
   if (p->stage_threads == 0) return false;
   const size_t bytes = p->chunk_stripes * (p->k + p->m) * p->bs;
-  for (auto& st : p->stage) {
+  for (size_t b = 0; b < p->stage_buffers; ++b) {
+    auto& st = p->stage[b];
     if (st.host == nullptr &&
         hipHostMalloc(reinterpret_cast<void**>(&st.host), bytes, hipHostMallocDefault) !=
             hipSuccess) {
@@ -369,7 +372,7 @@ bool ensure_stage(xec_pipeline* p) {
   }
   if (p->pool == nullptr) {
     try {  // no exception crosses the C ABI (a thread may fail to start)
-      p->pool = new HostPool(p->device, p->stage_threads, 2);
+      p->pool = new HostPool(p->device, p->stage_threads, p->stage_buffers);
     } catch (...) {
       p->pool = nullptr;
     }
@@ -451,7 +454,7 @@ struct InRun {
 };
 
 // A chunk's inputs, staged or not.  Staged runs (source in pageable memory)
-// are first copied by the pool into staging buffer `chunk_no % 2` at the
+// are first copied by the pool into staging buffer `chunk_no % nb_` at the
 // slot's offsets (`prefetch`, while the previous chunk's DMA runs); `issue`
 // then queues every run on the slot's stream -- staged ones from the staging
 // buffer, the rest straight from the caller's pinned memory -- and marks the
@@ -463,14 +466,17 @@ class Inputs {
   Inputs(xec_pipeline* p, bool stage_data, bool stage_parity, bool serial_auto = false)
       : p_(p), sd_(stage_data), sp_(stage_parity),
         serial_(p->opt_serial < 0 ? serial_auto : p->opt_serial == 1),
-        parity_at_(p->chunk_stripes * p->k * p->bs) {
+        parity_at_(p->chunk_stripes * p->k * p->bs), nb_(p->stage_buffers) {
     p->in_recorded = false;  // a new call: nothing of its own to wait for yet
   }
   bool staged() const { return sd_ || sp_; }
+  // how many chunks ahead the pool stages: one per staging buffer but the
+  // one the DMA is reading
+  size_t ahead() const { return staged() ? nb_ - 1 : 0; }
   template <typename Runs>
   void prefetch(size_t chunk_no, Runs&& runs) {
     if (!staged()) return;
-    auto& st = p_->stage[chunk_no % 2];
+    auto& st = p_->stage[chunk_no % nb_];
     std::vector<HostPool::Piece> pieces;
     runs([&](const InRun& r) {
       if (r.parity ? sp_ : sd_)
@@ -478,15 +484,15 @@ class Inputs {
       return true;
     });
     hipEvent_t after = st.recorded ? st.read : nullptr;
-    failed_[chunk_no % 2] = false;
+    failed_[chunk_no % nb_] = false;
     if (after != nullptr && p_->opt_main) {
       if (hipEventSynchronize(after) != hipSuccess) {  // issue() then fails
         pieces.clear();
-        failed_[chunk_no % 2] = true;
+        failed_[chunk_no % nb_] = true;
       }
       after = nullptr;
     }
-    p_->pool->submit(chunk_no % 2, after, pieces);
+    p_->pool->submit(chunk_no % nb_, after, pieces);
   }
   // `direct`: this chunk's runs all read the caller's memory on the slot's
   // stream (HIP stages pageable ones) -- the first chunk of a call, so that
@@ -508,8 +514,8 @@ class Inputs {
         return hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, r.src, r.bytes,
                               hipMemcpyHostToDevice, s.stream) == hipSuccess;
       });
-    auto& st = p_->stage[chunk_no % 2];
-    if (!p_->pool->wait(chunk_no % 2) || failed_[chunk_no % 2]) return false;
+    auto& st = p_->stage[chunk_no % nb_];
+    if (!p_->pool->wait(chunk_no % nb_) || failed_[chunk_no % nb_]) return false;
     // the runs alternate between the slot's stream and its aux stream, so one
     // copy's start-up hides behind the other's transfer; aux first waits until
     // the slot's stream is done with the slot's previous chunk, and the slot's
@@ -541,7 +547,8 @@ class Inputs {
   xec_pipeline* p_;
   bool sd_, sp_, serial_;
   size_t parity_at_;
-  bool failed_[2] = {false, false};
+  size_t nb_;
+  bool failed_[xec_pipeline::kMaxStage] = {};
 };
 
 }  // namespace
@@ -569,6 +576,8 @@ static xec_status create_impl(xec_pipeline** out, size_t chunk_stripes, size_t b
     p->opt_main = o.find('m') != std::string::npos;
     p->opt_encode = o.find('e') != std::string::npos;
     p->opt_serial = o.find('s') != std::string::npos ? 1 : o.find('n') != std::string::npos ? 0 : -1;
+    for (char c : o)
+      if (c >= '2' && c <= '4') p->stage_buffers = (size_t)(c - '0');
   }
   p->chunk_stripes = chunk_stripes;
   p->bs = bs;
@@ -640,13 +649,14 @@ static xec_status encode_impl(xec_pipeline* p, const void* h_data, void* h_parit
   const size_t chunks = (S + cs - 1) / cs;
   // the first chunk comes in directly (opt_first) while the pool stages the next
   const size_t first = in.staged() && p->opt_first ? 1 : 0;
-  if (first < chunks) in.prefetch(first, runs(first));
+  for (size_t q = first; q < chunks && q < first + in.ahead(); ++q) in.prefetch(q, runs(q));
   for (size_t chunk = 0; chunk < chunks; ++chunk) {
     const size_t n = (S - chunk * cs) < cs ? (S - chunk * cs) : cs;
     auto& s = p->slots[chunk % ns];
     // stream order serialises reuse of this slot behind its previous chunk
     if (!in.issue(chunk, s, runs(chunk), chunk < first)) return fail(p, XEC_DEVICE_ERROR);
-    if (chunk >= first && chunk + 1 < chunks) in.prefetch(chunk + 1, runs(chunk + 1));
+    const size_t next = chunk + in.ahead();
+    if (chunk >= first && next < chunks) in.prefetch(next, runs(next));
     xec_status st = xec_encode(s.data, s.parity, n, bs, k, m, s.stream);
     if (st != XEC_SUCCESS) return fail(p, st);
     if (defer ? (chunk > 0 && !out(chunk - 1)) : !out(chunk)) return fail(p, XEC_DEVICE_ERROR);
@@ -761,7 +771,8 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
   // the first rebuilding chunk comes in directly (opt_first) while the pool
   // stages the next
   const size_t first = in.staged() && p->opt_first ? 1 : 0;
-  if (first < work.size()) in.prefetch(first, runs(work[first], whole_chunks));
+  for (size_t q = first; q < work.size() && q < first + in.ahead(); ++q)
+    in.prefetch(q, runs(work[q], whole_chunks));
   for (size_t u = 0; u < work.size(); ++u) {
     const size_t chunk = work[u], c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
     const size_t slot = u % ns;
@@ -769,7 +780,8 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
     const bool direct = u < first;
     if (!in.issue(u, s, runs(chunk, direct ? whole_direct : whole_chunks), direct))
       return fail(p, XEC_DEVICE_ERROR);
-    if (u >= first && u + 1 < work.size()) in.prefetch(u + 1, runs(work[u + 1], whole_chunks));
+    const size_t next = u + in.ahead();
+    if (u >= first && next < work.size()) in.prefetch(next, runs(work[next], whole_chunks));
     st = xec_decode(s.data, s.parity, n, bs, k, m, h_bitmap + c0 * row, s.bitmap, s.stream);
     if (st != XEC_SUCCESS) return fail(p, st);
     if (!defer) {
