@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -242,7 +243,10 @@ struct xec_pipeline {
   unsigned stage_threads = 0;
   // XEC_PIPELINE_STAGE_OPTS (A/B): 'a' alternate H2D streams, 'f' first
   // chunk direct, 'm' main thread waits for the buffer, 'e' stage encode data
-  bool opt_aux = true, opt_first = true, opt_main = false, opt_encode = true;
+  // 'a' is off by default: a long fuzz sequence (tools/fuzz_big.py --pipeline
+  // --seed 90002, case 7) ended with a device error under it (profiles/r04q,
+  // r04r), and without it the same sequence passes
+  bool opt_aux = false, opt_first = true, opt_main = false, opt_encode = true;
   // Serial inputs: each chunk's H2D copies start only after the previous
   // chunk's are done (one input transfer in flight at a time).  Measured
   // (tools/pageable_probe.py, profiles/r04m/staging_default.json, 3 rounds):
@@ -408,10 +412,24 @@ struct DeviceGuard {
 
 // Error exit: drain what was already queued so no copy touches the caller's
 // buffers after the call returns.
-xec_status fail(xec_pipeline* p, xec_status st) {
+// XEC_PIPELINE_DEBUG=1: a failed call names its line and the HIP error
+// pending at that point on stderr (diagnostics only).
+bool debug_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("XEC_PIPELINE_DEBUG");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
+xec_status fail_at(xec_pipeline* p, xec_status st, int line) {
+  if (debug_on())
+    std::fprintf(stderr, "xec_pipeline: status %d at xec_pipeline.cpp:%d, pending HIP error %s\n",
+                 (int)st, line, hipGetErrorName(hipPeekAtLastError()));
   (void)sync_all(p);
   return st;
 }
+#define fail(p, st) fail_at((p), (st), __LINE__)
 
 // Copy runs of consecutive indices i < n with want(i) -- adjacent blocks merge
 // into one copy.
@@ -522,14 +540,20 @@ class Inputs {
     // stream then waits for aux
     hipStream_t other = s.aux != nullptr ? s.aux : s.stream;
     if (other != s.stream && (hipEventRecord(s.free_ev, s.stream) != hipSuccess ||
-                              hipStreamWaitEvent(other, s.free_ev, 0) != hipSuccess))
+                              hipStreamWaitEvent(other, s.free_ev, 0) != hipSuccess)) {
+      if (debug_on()) std::fprintf(stderr, "xec_pipeline: aux wait failed\n");
       return false;
+    }
     size_t n = 0;
     bool ok = runs([&](const InRun& r) {
       const bool from_stage = r.parity ? sp_ : sd_;
       const uint8_t* src = from_stage ? st.host + (r.parity ? parity_at_ : 0) + r.off : r.src;
-      return hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, src, r.bytes,
-                            hipMemcpyHostToDevice, (n++ % 2) ? other : s.stream) == hipSuccess;
+      const hipError_t e = hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, src, r.bytes,
+                                          hipMemcpyHostToDevice, (n++ % 2) ? other : s.stream);
+      if (e != hipSuccess && debug_on())
+        std::fprintf(stderr, "xec_pipeline: staged H2D of %zu bytes (run %zu) failed: %s\n",
+                     r.bytes, n - 1, hipGetErrorName(e));
+      return e == hipSuccess;
     });
     if (other != s.stream)
       ok = (hipEventRecord(s.aux_done, other) == hipSuccess &&

@@ -79,6 +79,9 @@ def main():
     ap.add_argument("--cases", type=int, default=60)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--pipeline", action="store_true")
+    ap.add_argument("--start", type=int, default=0,
+                    help="--pipeline: draw but skip the cases before this one (re-run one case "
+                         "of a seed's sequence)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -201,6 +204,11 @@ def pipeline_fuzz(args, np, torch, xec, s, rng):
         ns = int(rng.integers(1, 5))
         kind = ["uniform", "sparse", "skewed", "parity"][case % 4]
         unrec = case % 7 == 3
+        if case < args.start:  # advance the generator exactly as the case would
+            loss_pattern(np, rng, S, k, m, kind)
+            if unrec:
+                rng.integers(0, S)
+            continue
         d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
         p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
         assert xec.fill_splitmix64(d, S, k * bs, 9000 + case, s) == 0
@@ -237,6 +245,19 @@ def pipeline_fuzz(args, np, torch, xec, s, rng):
             dec_ok = st == 0 and bool(torch.equal(h_d, ref_d))
         else:
             dec_ok = st == 4 and bool(torch.equal(h_d, erased))
+        if not dec_ok:  # where: which stripes / blocks, lost or not, zero or stale
+            got = h_d.numpy().reshape(S, k, bs)
+            want = (ref_d if rec.all() else erased).numpy().reshape(S, k, bs)
+            bad = np.argwhere((got != want).any(axis=2))
+            print("diagnose " + json.dumps({
+                "status": st, "bad_blocks": int(len(bad)), "first_bad": bad[:12].tolist(),
+                "bad_chunks": sorted(set((bad[:, 0] // chunk).tolist()))[:24],
+                "bad_were_lost": int((bm[bad[:, 0], bad[:, 1]] == 0).sum()),
+                "bad_zero": int(sum((got[c, i] == 0).all() for c, i in bad[:200])),
+                "bad_eq_erased": int(sum((got[c, i] == erased.numpy().reshape(S, k, bs)[c, i]).all()
+                                         for c, i in bad[:200])),
+                "parity_intact": bool(torch.equal(h_p, ref_p)),
+                "chunks_total": (S + chunk - 1) // chunk}), flush=True)
         row = {"case": case, "k": k, "m": m, "bs": bs, "S": S, "chunk": chunk, "streams": ns,
                "MiB": round(S * k * bs / 2**20, 1), "pattern": kind, "host_memory": mem,
                "recoverable": bool(rec.all()), "encode_ok": enc_ok, "decode_ok": dec_ok}
