@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -121,21 +122,54 @@ struct Staging {
   void* host = nullptr;
   size_t cap = 0;
   int device = -1;
-  hipEvent_t done = nullptr;
+  hipEvent_t done = nullptr;     // on a library stream: the buffer's last reader has passed
+  hipEvent_t handoff = nullptr;  // throw-away record on the caller's stream (record_after)
   bool busy = false;
 };
 constexpr size_t kMaxStaging = 64;
 std::mutex g_stage_mu;
 std::vector<Staging*> g_stage;
 
-// hipEventQuery on a buffer's event: true once the work it marks has passed.
-// Only hipErrorNotReady means "not yet"; it is cleared so that no later
-// hipGetLastError reads it as a launch failure.  Any other error is left for
-// the caller to read and the buffer counts as in use.
+// hipEventQuery on a buffer's event (recorded on a stream the library owns,
+// track_stream below): true once the work it marks has passed.  The event is
+// the library's, so whatever its query raises -- hipErrorNotReady, "not yet",
+// or anything else, which keeps the buffer counted as in use -- is cleared,
+// unless an error of the caller's was already pending (then nothing is
+// touched).
 bool event_passed(hipEvent_t e) {
+  const bool clean = hipPeekAtLastError() == hipSuccess;
   const hipError_t q = hipEventQuery(e);
-  if (q == hipErrorNotReady) (void)hipGetLastError();
+  if (q != hipSuccess && clean) (void)hipGetLastError();
   return q == hipSuccess;
+}
+
+// A buffer read by the caller's stream is free once that stream has passed
+// the reading work -- but an event recorded on the CALLER's stream may outlive
+// that stream (a pipeline destroys its streams), and querying it later made
+// HIP report a stray error (hipErrorStreamCaptureUnsupported, read by the
+// next launch's hipGetLastError: tools/fuzz_big.py --pipeline, profiles/r04s).
+// So the caller's stream only hands over to a per-device tracking stream of
+// the library's (hipStreamWaitEvent on a throw-away record), and the buffer's
+// event is recorded there (g_track_mu guards the stream list).
+std::mutex g_track_mu;
+std::vector<std::pair<int, hipStream_t>> g_track_streams;
+hipStream_t track_stream(int dev) {
+  std::lock_guard<std::mutex> lk(g_track_mu);
+  for (auto& ts : g_track_streams)
+    if (ts.first == dev) return ts.second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  g_track_streams.emplace_back(dev, s);
+  return s;
+}
+
+// Record `done` once `caller` has passed its current work, on the library's
+// tracking stream of `dev` (`handoff` is the throw-away record on the caller's
+// stream); false if that cannot be queued.
+bool record_after(hipEvent_t done, hipEvent_t handoff, hipStream_t caller, int dev) {
+  const hipStream_t ts = track_stream(dev);
+  return ts != nullptr && hipEventRecord(handoff, caller) == hipSuccess &&
+         hipStreamWaitEvent(ts, handoff, 0) == hipSuccess && hipEventRecord(done, ts) == hipSuccess;
 }
 
 // The slot is picked and marked busy under the lock; waiting for a recycled
@@ -162,7 +196,9 @@ Staging* stage_acquire(size_t bytes, int dev) {
     if (pick == nullptr) {
       pick = new Staging;
       pick->device = dev;
-      if (hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {
+      if (hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&pick->handoff, hipEventDisableTiming) != hipSuccess) {
+        if (pick->done) (void)hipEventDestroy(pick->done);
         delete pick;
         return nullptr;
       }
@@ -175,7 +211,10 @@ Staging* stage_acquire(size_t bytes, int dev) {
     pick->busy = false;
     return nullptr;
   };
-  if (recycled && hipEventSynchronize(pick->done) != hipSuccess) return give_back();
+  if (recycled && hipEventSynchronize(pick->done) != hipSuccess) {
+    (void)hipGetLastError();  // the library's own event
+    return give_back();
+  }
   if (pick->cap < bytes) {
     if (pick->host != nullptr) (void)hipHostFree(pick->host);
     pick->host = nullptr;
@@ -192,11 +231,12 @@ Staging* stage_acquire(size_t bytes, int dev) {
 }
 
 // `stream` = where a copy from the buffer was queued (nullptr-able), or
-// `queued` = false when nothing was.  If the event cannot be recorded there
-// (a stream of another device than the one current when the buffer was
-// made), the copy is waited for instead, so the buffer is never reused early.
-void stage_release(Staging* st, bool queued, hipStream_t stream) {
-  if (queued && hipEventRecord(st->done, stream) != hipSuccess)
+// `queued` = false when nothing was; `own`: the stream is the library's (its
+// copy stream), else the caller's (record_after).  If the event cannot be
+// recorded, the copy is waited for instead, so the buffer is never reused early.
+void stage_release(Staging* st, bool queued, hipStream_t stream, bool own) {
+  if (queued && !(own ? hipEventRecord(st->done, stream) == hipSuccess
+                      : record_after(st->done, st->handoff, stream, st->device)))
     (void)hipStreamSynchronize(stream);
   std::lock_guard<std::mutex> lk(g_stage_mu);
   st->busy = false;
@@ -221,7 +261,8 @@ struct DevSlot {
   size_t cap = 0;
   int device = -1;
   hipEvent_t copied = nullptr;  // on the copy stream, after the upload
-  hipEvent_t done = nullptr;    // on the caller's stream, after the reading kernel
+  hipEvent_t done = nullptr;    // on a library stream, after the reading kernel (record_after)
+  hipEvent_t handoff = nullptr;  // throw-away record on the caller's stream
   bool busy = false;
 };
 constexpr size_t kMaxSlots = 16;
@@ -269,7 +310,11 @@ bool side_uploads() {
 int stream_busy(hipStream_t stream) {
   const hipError_t q = hipStreamQuery(stream);
   if (q == hipSuccess) return 0;
-  if (q != hipErrorNotReady) return -1;
+  if (q != hipErrorNotReady) {
+    if (const char* e = std::getenv("XEC_DEBUG"); e != nullptr && e[0] == '1')
+      std::fprintf(stderr, "xec: hipStreamQuery: %s\n", hipGetErrorName(q));
+    return -1;
+  }
   (void)hipGetLastError();
   return 1;
 }
@@ -340,8 +385,10 @@ bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
       pick = new DevSlot;
       pick->device = dev;
       if (hipEventCreateWithFlags(&pick->copied, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {
+          hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&pick->handoff, hipEventDisableTiming) != hipSuccess) {
         if (pick->copied) (void)hipEventDestroy(pick->copied);
+        if (pick->done) (void)hipEventDestroy(pick->done);
         delete pick;
         return false;
       }
@@ -354,7 +401,10 @@ bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
     pick->busy = false;
     return false;
   };
-  if (recycled && hipEventSynchronize(pick->done) != hipSuccess) return give_back();
+  if (recycled && hipEventSynchronize(pick->done) != hipSuccess) {
+    (void)hipGetLastError();  // the library's own event
+    return give_back();
+  }
   if (pick->cap < bytes) {
     if (pick->dev != nullptr) (void)hipFree(pick->dev);
     pick->dev = nullptr;
@@ -390,7 +440,9 @@ bool upload_join(const Upload& up, hipStream_t stream) {
 void upload_end(Upload& up, hipStream_t stream, bool launched) {
   if (up.slot == nullptr) return;
   hipStream_t after = launched ? stream : up.cs;
-  if (hipEventRecord(up.slot->done, after) != hipSuccess) (void)hipStreamSynchronize(after);
+  const bool ok = launched ? record_after(up.slot->done, up.slot->handoff, stream, up.slot->device)
+                           : hipEventRecord(up.slot->done, up.cs) == hipSuccess;
+  if (!ok) (void)hipStreamSynchronize(after);
   std::lock_guard<std::mutex> lk(g_slot_mu);
   up.slot->busy = false;
   up.slot = nullptr;
@@ -534,6 +586,24 @@ constexpr size_t kCopyFirstBitmapBytes = 256u << 10;
 // against the better of them, profiles/r02n/tiling_uniform.json, r02o).
 constexpr uint64_t kListStripesNum = 3, kListStripesDen = 4;
 
+// XEC_DEBUG=1: a decode that fails with XEC_DEVICE_ERROR names its line, the
+// HIP error of the failing call and the one pending on the thread (stderr;
+// diagnostics only).
+static bool debug_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("XEC_DEBUG");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+static xec_status dev_error(int line, hipError_t e) {
+  if (debug_on())
+    std::fprintf(stderr, "xec: device error at xec_api.cpp:%d (%s; pending %s)\n", line,
+                 hipGetErrorName(e), hipGetErrorName(hipPeekAtLastError()));
+  return XEC_DEVICE_ERROR;
+}
+#define DEVERR(e) dev_error(__LINE__, (e))
+
 static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                               size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
                               hipStream_t stream) {
@@ -558,10 +628,10 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   if (!copy_first) {
     st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
     if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) return st;
-    if (cap || capturing(stream)) return XEC_DEVICE_ERROR;
+    if (cap || capturing(stream)) return DEVERR(hipSuccess);
   }
   const StreamDevice sd(stream);
-  if (!sd.ok()) return XEC_DEVICE_ERROR;
+  if (!sd.ok()) return DEVERR(hipSuccess);
   const int dev = sd.device();
   // Whether uploads go off the stream, asked (hipStreamQuery) only when
   // something is about to be uploaded: a list that travels in the kernel
@@ -588,7 +658,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
            hipSuccess;
   };
   if (copy_first) {
-    if (!upload_bitmap()) return XEC_DEVICE_ERROR;
+    if (!upload_bitmap()) return DEVERR(hipSuccess);
     st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, nullptr, 0);
     if (st != XEC_SUCCESS || !scan.needs_recovery || scan.lost_data == 0) {
       upload_end(bmu, stream, false);  // only the bitmap copy was queued
@@ -617,10 +687,10 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, items, xec::kArgItems);
       if (st != XEC_SUCCESS) return st;
       g_tiling_used = XEC_TILING_ARG_LIST;
-      return xec::launch_decode(d_data, d_parity, nullptr, g, ls, xec::kDecodeArgListTiles,
-                                stream, scan.lost_data, items) == hipSuccess
-                 ? XEC_SUCCESS
-                 : XEC_DEVICE_ERROR;
+      const hipError_t le = xec::launch_decode(d_data, d_parity, nullptr, g, ls,
+                                               xec::kDecodeArgListTiles, stream, scan.lost_data,
+                                               items);
+      return le == hipSuccess ? XEC_SUCCESS : DEVERR(le);
     }
     // u32 entries staged in pinned host memory by the listing pass, then
     // uploaded: to a library buffer off the stream, or into the 4-byte-aligned
@@ -632,44 +702,46 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
     const bool off_stream = side();
     if (query_failed) {
       upload_end(bmu, stream, false);
-      return XEC_DEVICE_ERROR;
+      return DEVERR(hipSuccess);
     }
     if (off_stream || n <= cap) sg = stage_acquire(n * 4, dev);
     if (sg != nullptr) {
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, static_cast<uint32_t*>(sg->host), n);
       if (st != XEC_SUCCESS) {
-        stage_release(sg, false, stream);
+        stage_release(sg, false, stream, false);
         upload_end(bmu, stream, false);
         return st;
       }
       Upload lu;
       bool ok = true;
       if (side() && upload_begin(sg->host, n * 4, dev, lu)) {
-        stage_release(sg, true, lu.cs);
+        stage_release(sg, true, lu.cs, true);
         ok = upload_join(lu, stream);
       } else if (n <= cap) {
         // stream-ordered after any bitmap copy into the same scratch
         lu.dev = d_bitmap + pad;
         ok = hipMemcpyAsync(lu.dev, sg->host, n * 4, hipMemcpyHostToDevice, stream) == hipSuccess;
-        stage_release(sg, ok, stream);
+        stage_release(sg, ok, stream, false);
       } else {
-        stage_release(sg, false, stream);  // denser than the scratch holds: bitmap tiles
+        stage_release(sg, false, stream, false);  // denser than the scratch holds: bitmap tiles
       }
       if (lu.dev != nullptr) {
         upload_end(bmu, stream, false);
         g_tiling_used = XEC_TILING_LIST;
-        ok = ok && xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,
-                                      stream, n) == hipSuccess;
+        const hipError_t le =
+            ok ? xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,
+                                    stream, n)
+               : hipErrorUnknown;
         upload_end(lu, stream, true);
-        return ok ? XEC_SUCCESS : XEC_DEVICE_ERROR;
+        return le == hipSuccess ? XEC_SUCCESS : DEVERR(le);
       }
     }
     // no staging memory, or a list denser than the scratch holds: bitmap tiles
   }
-  if (!copy_first && !upload_bitmap()) return XEC_DEVICE_ERROR;
+  if (!copy_first && !upload_bitmap()) return DEVERR(hipSuccess);
   if (!upload_join(bmu, stream)) {
     upload_end(bmu, stream, false);
-    return XEC_DEVICE_ERROR;
+    return DEVERR(hipSuccess);
   }
   // class tiles: one reduction per tile, so the encode's residency table
   xec::LaunchShape ls = launch_shape(
@@ -677,11 +749,11 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   ls.rot = decode_rotation(scan, m, bs);
   const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
   g_tiling_used = cls && m > 1 ? XEC_TILING_CLASS : XEC_TILING_STRIPE;
-  const bool ok = xec::launch_decode(d_data, d_parity, bmu.dev, g, ls,
-                                     cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
-                                     stream) == hipSuccess;
+  const hipError_t le = xec::launch_decode(d_data, d_parity, bmu.dev, g, ls,
+                                           cls ? xec::kDecodeClassTiles : xec::kDecodeStripeTiles,
+                                           stream);
   upload_end(bmu, stream, true);
-  return ok ? XEC_SUCCESS : XEC_DEVICE_ERROR;
+  return le == hipSuccess ? XEC_SUCCESS : DEVERR(le);
 }
 
 // No exception crosses the C ABI: the host-side bookkeeping allocates (upload
@@ -747,7 +819,7 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
   g_tiling_used = XEC_TILING_LIST;
   Upload lu;
   if (busy == 1 && upload_begin(items, n * 4, dev, lu)) {
-    stage_release(sg, true, lu.cs);
+    stage_release(sg, true, lu.cs, true);
     const bool ok = upload_join(lu, stream) &&
                     xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,
                                        stream, n) == hipSuccess;
@@ -766,7 +838,7 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
     ok = ok && xec::launch_decode(d_data, d_parity, d_items, g, ls, xec::kDecodeListTiles, stream,
                                   piece) == hipSuccess;
   }
-  stage_release(sg, queued, stream);
+  stage_release(sg, queued, stream, false);
   return ok ? verdict : XEC_DEVICE_ERROR;
 }
 

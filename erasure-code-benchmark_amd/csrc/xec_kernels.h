@@ -56,6 +56,15 @@ inline uint32_t grid_for(uint64_t work_items, uint32_t max_grid, uint32_t thread
   return (uint32_t)(grid ? grid : 1);
 }
 
+// The status of the launch(es) a wrapper just made: the error pending now,
+// unless it is the one already pending before them (`before`, an earlier
+// call's -- the caller's to read, so it is neither reported nor cleared here).
+inline hipError_t launch_status(hipError_t before) {
+  const hipError_t now = hipPeekAtLastError();
+  if (now == hipSuccess || now == before) return hipSuccess;
+  return hipGetLastError();
+}
+
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
                          const LaunchShape& ls, hipStream_t s);
 // Decode tilings.  Stripe: one tile per (stripe, chunk), d_bitmap = the batch

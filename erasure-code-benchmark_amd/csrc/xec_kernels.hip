@@ -471,15 +471,17 @@ namespace {
 template <int NM, int U, bool NT, int T>
 hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t grid,
                            uint32_t lds, hipStream_t s) {
+  const hipError_t before = hipPeekAtLastError();
   encode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<const uint8_t*>(d),
                                                  static_cast<uint8_t*>(p), g);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
                            int tiling, uint32_t grid, uint32_t lds, hipStream_t s,
                            const ArgItems* args) {
+  const hipError_t before = hipPeekAtLastError();
   if (tiling == kDecodeDevListTiles)
     decode_devlist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
         static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p),
@@ -497,7 +499,7 @@ hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geom
   else
     decode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<uint8_t*>(d),
                                                    static_cast<const uint8_t*>(p), bm, g);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 // Member counts (k/m) compiled fully unrolled: those of the reference's sweep
@@ -591,37 +593,41 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
 
 hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
                         hipStream_t s) {
+  const hipError_t before = hipPeekAtLastError();
   const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
   check_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 hipError_t launch_scan_list(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
                             uint32_t* d_list, hipStream_t s) {
+  const hipError_t before = hipPeekAtLastError();
   reset_status_list_kernel<<<1, 1, 0, s>>>(d_status, d_list);
   const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
   scan_list_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status, d_list);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, const Geometry& g,
                         hipStream_t s) {
+  const hipError_t before = hipPeekAtLastError();
   const uint64_t nblocks = g.S * (g.k + g.m);
   const uint32_t grid = grid_for(nblocks, 65536, 256);
   erase_kernel<<<grid, 256, 0, s>>>(static_cast<uint8_t*>(d_data), static_cast<uint8_t*>(d_parity),
                                     d_bitmap, g);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,
                        hipStream_t s) {
+  const hipError_t before = hipPeekAtLastError();
   uint64_t gx = (words + 255) / 256;
   if (gx > 1024) gx = 1024;
   const uint64_t gy = S < 65535 ? S : 65535;
   if (gx == 0 || gy == 0) return hipSuccess;
   fill_kernel<<<dim3((uint32_t)gx, (uint32_t)gy), 256, 0, s>>>(static_cast<uint64_t*>(d_buf), S,
                                                               words, seed_base);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 // Loads this file's code object onto the current device (see xec_kernels.h).

@@ -404,6 +404,7 @@ thread_local int g_validate_mode = 0;  // 0 auto, 1 lane, 2 grouped (xec_set_val
 
 hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t seed,
                           hipStream_t s) {
+  const hipError_t before = hipPeekAtLastError();
   if (nblocks == 0) return hipSuccess;
   uint8_t* d = static_cast<uint8_t*>(d_data);
   const int g = group_lanes(bs);
@@ -414,11 +415,12 @@ hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t 
     launch_grouped<PatternK>(g, nblocks, s, d, nblocks, bs, seed);
   else
     serial_pattern_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(d, nblocks, bs, seed);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, uint32_t* d_bad,
                            hipStream_t s) {
+  const hipError_t before = hipPeekAtLastError();
   if (hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
   if (nblocks == 0) return hipSuccess;
   const uint8_t* d = static_cast<const uint8_t*>(d_data);
@@ -430,7 +432,7 @@ hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, ui
   else
     serial_validate_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(d, nblocks, bs,
                                                                             d_bad);
-  return hipGetLastError();
+  return launch_status(before);
 }
 
 // Loads this file's code object onto the current device (see xec_kernels.h).
