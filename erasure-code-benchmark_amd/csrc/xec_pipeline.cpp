@@ -243,10 +243,10 @@ struct xec_pipeline {
   unsigned stage_threads = 0;
   // XEC_PIPELINE_STAGE_OPTS (A/B): 'a' alternate H2D streams, 'f' first
   // chunk direct, 'm' main thread waits for the buffer, 'e' stage encode data
-  // 'a' is off by default: a long fuzz sequence (tools/fuzz_big.py --pipeline
-  // --seed 90002, case 7) ended with a device error under it (profiles/r04q,
-  // r04r), and without it the same sequence passes
-  bool opt_aux = false, opt_first = true, opt_main = false, opt_encode = true;
+  // (a fuzz sequence that ended in a device error with 'a' -- profiles/r04q,
+  // r04r -- turned out to be the library's buffer events on destroyed caller
+  // streams, csrc/xec_api.cpp record_after; 300 fuzz cases pass since, r04u)
+  bool opt_aux = true, opt_first = true, opt_main = false, opt_encode = true;
   // Serial inputs: each chunk's H2D copies start only after the previous
   // chunk's are done (one input transfer in flight at a time).  Measured
   // (tools/pageable_probe.py, profiles/r04m/staging_default.json, 3 rounds):
