@@ -247,6 +247,7 @@ struct xec_pipeline {
   // r04r -- turned out to be the library's buffer events on destroyed caller
   // streams, csrc/xec_api.cpp record_after; 300 fuzz cases pass since, r04u)
   bool opt_aux = true, opt_first = true, opt_main = false, opt_encode = true;
+  bool opt_pinned_aux = false;  // 'p' (A/B): pinned inputs alternate over the two streams too
   // Serial inputs: each chunk's H2D copies start only after the previous
   // chunk's are done (one input transfer in flight at a time).  Measured
   // (tools/pageable_probe.py, profiles/r04m/staging_default.json, 3 rounds):
@@ -344,6 +345,22 @@ bool ensure_bounce(xec_pipeline* p) {
   return p->copier != nullptr;
 }
 
+// Each slot's second stream for input copies and its two events.
+bool ensure_aux(xec_pipeline* p) {
+  for (auto& s : p->slots) {
+    if (s.aux == nullptr && hipStreamCreateWithFlags(&s.aux, hipStreamNonBlocking) != hipSuccess) {
+      s.aux = nullptr;
+      return false;
+    }
+    for (hipEvent_t* e : {&s.free_ev, &s.aux_done})
+      if (*e == nullptr && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+        *e = nullptr;
+        return false;
+      }
+  }
+  return true;
+}
+
 // Staging buffers, their events and the pool, for inputs from pageable
 // memory; false if any of them cannot be had (or staging is off).
 bool ensure_stage(xec_pipeline* p) {
@@ -362,18 +379,7 @@ bool ensure_stage(xec_pipeline* p) {
       return false;
     }
   }
-  for (auto& s : p->slots) {
-    if (!p->opt_aux) break;
-    if (s.aux == nullptr && hipStreamCreateWithFlags(&s.aux, hipStreamNonBlocking) != hipSuccess) {
-      s.aux = nullptr;
-      return false;
-    }
-    for (hipEvent_t* e : {&s.free_ev, &s.aux_done})
-      if (*e == nullptr && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
-        *e = nullptr;
-        return false;
-      }
-  }
+  if (p->opt_aux && !ensure_aux(p)) return false;
   if (p->pool == nullptr) {
     try {  // no exception crosses the C ABI (a thread may fail to start)
       p->pool = new HostPool(p->device, p->stage_threads, p->stage_buffers);
@@ -527,17 +533,36 @@ class Inputs {
  private:
   template <typename Runs>
   bool issue_impl(size_t chunk_no, xec_pipeline::Slot& s, Runs&& runs, bool direct) {
-    if (!staged() || direct)
+    if (!staged() || direct) {
+      if (!staged() && p_->opt_pinned_aux && s.aux != nullptr)  // 'p': pinned inputs alternate
+        return alternate(s, runs, [](const InRun& r) { return r.src; });
       return runs([&](const InRun& r) {
         return hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, r.src, r.bytes,
                               hipMemcpyHostToDevice, s.stream) == hipSuccess;
       });
+    }
     auto& st = p_->stage[chunk_no % nb_];
     if (!p_->pool->wait(chunk_no % nb_) || failed_[chunk_no % nb_]) return false;
-    // the runs alternate between the slot's stream and its aux stream, so one
-    // copy's start-up hides behind the other's transfer; aux first waits until
-    // the slot's stream is done with the slot's previous chunk, and the slot's
-    // stream then waits for aux
+    const bool ok = alternate(s, runs, [&](const InRun& r) {
+      return (r.parity ? sp_ : sd_) ? st.host + (r.parity ? parity_at_ : 0) + r.off : r.src;
+    });
+    if (ok && hipEventRecord(st.read, s.stream) == hipSuccess) {
+      st.recorded = true;
+      return true;
+    }
+    if (s.aux) (void)hipStreamSynchronize(s.aux);  // nothing reads the buffer after this
+    (void)hipStreamSynchronize(s.stream);
+    st.recorded = false;
+    return false;
+  }
+
+  // The runs alternate between the slot's stream and its aux stream (when it
+  // has one), so one copy's start-up hides behind the other's transfer; aux
+  // first waits until the slot's stream is done with the slot's previous
+  // chunk, and the slot's stream then waits for aux.  `src_of(run)`: where
+  // the run's bytes are read from.
+  template <typename Runs, typename Src>
+  bool alternate(xec_pipeline::Slot& s, Runs&& runs, Src&& src_of) {
     hipStream_t other = s.aux != nullptr ? s.aux : s.stream;
     if (other != s.stream && (hipEventRecord(s.free_ev, s.stream) != hipSuccess ||
                               hipStreamWaitEvent(other, s.free_ev, 0) != hipSuccess)) {
@@ -546,26 +571,18 @@ class Inputs {
     }
     size_t n = 0;
     bool ok = runs([&](const InRun& r) {
-      const bool from_stage = r.parity ? sp_ : sd_;
-      const uint8_t* src = from_stage ? st.host + (r.parity ? parity_at_ : 0) + r.off : r.src;
-      const hipError_t e = hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, src, r.bytes,
-                                          hipMemcpyHostToDevice, (n++ % 2) ? other : s.stream);
+      const hipError_t e = hipMemcpyAsync((r.parity ? s.parity : s.data) + r.off, src_of(r),
+                                          r.bytes, hipMemcpyHostToDevice,
+                                          (n++ % 2) ? other : s.stream);
       if (e != hipSuccess && debug_on())
-        std::fprintf(stderr, "xec_pipeline: staged H2D of %zu bytes (run %zu) failed: %s\n",
-                     r.bytes, n - 1, hipGetErrorName(e));
+        std::fprintf(stderr, "xec_pipeline: H2D of %zu bytes (run %zu) failed: %s\n", r.bytes,
+                     n - 1, hipGetErrorName(e));
       return e == hipSuccess;
     });
     if (other != s.stream)
       ok = (hipEventRecord(s.aux_done, other) == hipSuccess &&
             hipStreamWaitEvent(s.stream, s.aux_done, 0) == hipSuccess) && ok;
-    if (ok && hipEventRecord(st.read, s.stream) == hipSuccess) {
-      st.recorded = true;
-      return true;
-    }
-    (void)hipStreamSynchronize(other);  // nothing reads the buffer after this
-    (void)hipStreamSynchronize(s.stream);
-    st.recorded = false;
-    return false;
+    return ok;
   }
 
   xec_pipeline* p_;
@@ -599,6 +616,7 @@ static xec_status create_impl(xec_pipeline** out, size_t chunk_stripes, size_t b
     p->opt_first = o.find('f') != std::string::npos;
     p->opt_main = o.find('m') != std::string::npos;
     p->opt_encode = o.find('e') != std::string::npos;
+    p->opt_pinned_aux = o.find('p') != std::string::npos;
     p->opt_serial = o.find('s') != std::string::npos ? 1 : o.find('n') != std::string::npos ? 0 : -1;
     for (char c : o)
       if (c >= '2' && c <= '4') p->stage_buffers = (size_t)(c - '0');
@@ -713,6 +731,7 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
   const bool paged_parity = !host_pinned(h_parity);
   if (pageable && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
   const bool stage = (pageable || paged_parity) && ensure_stage(p);
+  if (!stage && p->opt_pinned_aux) (void)ensure_aux(p);  // without: one stream, as before
   Inputs in(p, stage && pageable, stage && paged_parity);
   // (the first chunk of a staged call comes in directly, so whole too)
   const bool whole_direct = pageable && !selective;

@@ -103,7 +103,8 @@ def test_pipeline_decode_skipped_chunks_and_pageable(gpu, oracle, ns, lossy_chun
 @pytest.mark.parametrize("threads,opts", [("0", None), ("0", "s"), ("1", None), ("4", None),
                                           ("4", ""), ("4", "a"), ("4", "f"), ("4", "me"),
                                           ("4", "afe"), ("4", "afes"), ("4", "afen"),
-                                          ("4", "afe3"), ("2", "afe4")])
+                                          ("4", "afe3"), ("2", "afe4"), ("4", "afep"),
+                                          ("0", "p")])
 @pytest.mark.parametrize("pin_d,pin_p", [(False, False), (False, True), (True, False)])
 @pytest.mark.parametrize("S,k,m,bs,chunk,ns", [(37, 8, 1, 65536, 8, 3), (24, 16, 4, 65536, 5, 2),
                                               (30, 12, 4, 4096, 7, 1), (9, 8, 2, 1 << 20, 2, 3)])
@@ -114,7 +115,7 @@ def test_pipeline_staged_pageable_inputs(gpu, oracle, monkeypatch, threads, opts
     under every XEC_PIPELINE_STAGE_OPTS variant (a: copies alternate over two
     streams, f: first chunk direct, m: the calling thread waits for a buffer,
     e: encode data staged too, s / n: one chunk's input copies in flight at a time
-    always / never, a digit: staging buffers;
+    always / never, a digit: staging buffers, p: pinned inputs alternate too;
     unset = the library default): every mix of
     pinned and pageable data / parity, selective (m > 1, >= 64 KiB) and
     whole-run copies, one to three slots, ragged last chunk."""
