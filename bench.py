@@ -372,6 +372,36 @@ def _cpu_child(spec, env, timeout):
     return json.loads(lines[-1])
 
 
+PLACEMENTS = {"gpu_node_bound": None, "unbound": "unbound_diagnostic",
+              "all_nodes_bound": "all_nodes_diagnostic"}
+
+
+def pick_best_placement(out):
+    """`value` is the FASTEST placement of the same thread count that this run
+    measured (BASELINE.md §2 asks for `nproc` threads and no particular
+    binding; ADVICE r04: the GPU-node binding alone under-reported the host by
+    ~20 %).  The GPU-node-bound figure stays beside it as
+    `gpu_node_bound_diagnostic`, every placement's median in `placements`, and
+    `placement` names the headline.  by_workload / single_thread stay the
+    GPU-node-bound child's (the only one that times them)."""
+    cands = {"gpu_node_bound": out}
+    for name, key in PLACEMENTS.items():
+        d = out.get(key) if key else None
+        if isinstance(d, dict) and d.get("value"):
+            cands[name] = d
+    out["placements"] = {n: d["value"] for n, d in cands.items()}
+    best = max(cands, key=lambda n: cands[n]["value"])
+    out["placement"] = best
+    out["gpu_node_bound_diagnostic"] = {kx: out[kx] for kx in ("value", "min", "max", "samples")}
+    if best != "gpu_node_bound":
+        d = cands[best]
+        for kx in ("value", "min", "max", "samples"):
+            out[kx] = d[kx]
+        out["sample"] += (f"; value = the {best} placement of the same threads "
+                          f"(fastest of {sorted(cands)}), median of its samples")
+    return out
+
+
 def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, numa_node=None,
                  sample_bytes=CPU_SAMPLE_BYTES):
     """BASELINE.md §2 / SURVEY.md §8(d): the CPU XOR-EC path timed on this host's
@@ -383,13 +413,14 @@ def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, numa_node=None,
     mask, OMP_NUM_THREADS and the cgroup quota (16 on the GPU box: a 16-CPU
     quota over a 256-CPU mask) -- each bound to its own physical core on the
     GPU's NUMA node (cpu_places; OMP_PROC_BIND=close, OMP_PLACES), in a child
-    process so the OpenMP runtime starts with that binding.  `value` is the
-    median of CPU_SAMPLES samples (min / max beside it), plus 1 thread and the
-    other BASELINE shapes (`by_workload`).  The same threads UNBOUND
+    process so the OpenMP runtime starts with that binding: the median of
+    CPU_SAMPLES samples (min / max beside it), plus 1 thread and the other
+    BASELINE shapes (`by_workload`).  The same threads UNBOUND
     (OMP_PROC_BIND=false: the scheduler free to spread them over the whole
     mask, both sockets) are timed once more as `unbound_diagnostic` -- the
-    placement rounds 1-3 ran with, whose 318 / 382 / 478 GB/s spread this
-    separates from the codec.  Nothing built from the reference runs here."""
+    placement rounds 1-3 ran with -- and bound across every node as
+    `all_nodes_diagnostic`.  `value` is the fastest of the three
+    (pick_best_placement).  Nothing built from the reference runs here."""
     nproc, omp, quota = _host_threads()
     threads = max(1, min(x for x in (nproc, omp, int(quota) if quota else None) if x))
     cpus = cpu_places(threads, numa_node)
@@ -446,6 +477,7 @@ def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, numa_node=None,
                 "(every socket), not only the GPU's NUMA node")
         except (RuntimeError, OSError, ValueError) as e:  # diagnostic only
             out["all_nodes_diagnostic"] = {"error": repr(e)[:200]}
+    pick_best_placement(out)
     # BASELINE.md §2 names `nproc` threads: where the mask is wider than the
     # CPUs this process may use (256 vs a 16-CPU quota on the GPU box) that
     # count is timed too, unbound, beside the value

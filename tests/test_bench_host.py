@@ -37,7 +37,12 @@ def test_cpu_baseline_shape():
     assert len(out["samples"]) == bench.CPU_SAMPLES
     assert out["min"] <= out["value"] <= out["max"]
     assert set(out["by_workload"]) == {"cfg2", "cfg3", "cfg4"}
-    assert out["by_workload"]["cfg2"]["value"] == out["value"]
+    # value = the fastest measured placement of the same threads;
+    # by_workload comes from the GPU-node-bound child
+    assert out["by_workload"]["cfg2"]["value"] == out["gpu_node_bound_diagnostic"]["value"]
+    assert out["placement"] in out["placements"]
+    assert out["value"] == max(out["placements"].values())
+    assert out["placements"]["gpu_node_bound"] == out["gpu_node_bound_diagnostic"]["value"]
     for w in out["by_workload"].values():
         assert w["value"] > 0 and w["single_thread"]["value"] > 0 and w["min"] <= w["max"]
     nproc = len(os.sched_getaffinity(0))
