@@ -341,3 +341,42 @@ extern "C" xec_status xec_check_bitmap(const uint8_t* bm, size_t S, size_t k, si
   if (needs) *needs = r.needs_recovery;
   return st;
 }
+
+// The reference's erasure draw (select_lost_blocks, utils.cpp:100-127) with an
+// explicit seed (include/xec.h): PCG32 (PCGRandom, utils.cpp:17-32) seeded
+// RANDOM_SEED + seed on stream 1; each draw picks among the still-eligible
+// block indices in increasing order and retires the drawn block's parity
+// class.  The eligible list is compacted in place, so the draw sequence and
+// the index it selects match the reference's erase_if over its vector.
+extern "C" xec_status xec_select_lost_blocks(size_t k, size_t m, size_t lost, uint8_t* bm,
+                                             uint64_t seed) {
+  if (lost == 0) return XEC_SUCCESS;
+  if (m == 0 || lost > m) return XEC_INVALID_COUNTS;
+  if (bm == nullptr) return XEC_INVALID_SIZE;
+  constexpr uint64_t kRandomSeed = 1896;  // RANDOM_SEED, utils.hpp:26
+  uint64_t state = 0;
+  const uint64_t inc = (1ull << 1) | 1ull;
+  auto next = [&]() {
+    const uint64_t old = state;
+    state = old * 6364136223846793005ull + inc;
+    const uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = static_cast<uint32_t>(old >> 59u);
+    return (xs >> rot) | (xs << ((0u - rot) & 31u));
+  };
+  (void)next();
+  state += kRandomSeed + seed;
+  (void)next();
+  std::vector<uint32_t> eligible(k + m);
+  for (size_t i = 0; i < eligible.size(); ++i) eligible[i] = static_cast<uint32_t>(i);
+  size_t n = eligible.size();
+  for (size_t d = 0; d < lost; ++d) {
+    const uint32_t b = eligible[next() % n];
+    bm[b] = 0;
+    const size_t cls = b % m;
+    size_t w = 0;
+    for (size_t r = 0; r < n; ++r)
+      if (eligible[r] % m != cls) eligible[w++] = eligible[r];
+    n = w;
+  }
+  return XEC_SUCCESS;
+}

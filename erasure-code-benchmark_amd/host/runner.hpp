@@ -17,7 +17,8 @@
 #include <string>
 #include <vector>
 
-#include "abstract_bm.hpp"
+#include "abstract_bm.hpp"           // the plugin interface (integration/iface/)
+#include "xec_plugin_options.hpp"
 
 namespace xec {
 
@@ -53,29 +54,31 @@ inline Stats compute_stats(const std::vector<double>& t_ns, size_t data_bytes) {
 }
 
 template <typename Bench>
-RunResult run_generic(const std::string& name, const BenchmarkConfig& cfg) {
+RunResult run_generic(const std::string& name, const ::BenchmarkConfig& cfg,
+                      const XecPluginOptions& opt) {
   using clock = std::chrono::steady_clock;
   RunResult r;
   r.name = name;
-  Bench bench(cfg);
+  Bench bench(cfg, opt);
+  ::AbstractBenchmark& b = bench;  // driven through the interface only, as BM_generic
   for (int i = 0; i < cfg.num_warmup_iterations; ++i) {
-    bench.setup();
-    bench.encode();
-    bench.simulate_data_loss();
-    bench.decode();
+    b.setup();
+    b.encode();
+    b.simulate_data_loss();
+    b.decode();
   }
   std::vector<double> enc, dec;
   for (int i = 0; i < cfg.num_iterations; ++i) {
-    bench.setup();
+    b.setup();
     auto t0 = clock::now();
-    int rc = bench.encode();
+    int rc = b.encode();
     auto t1 = clock::now();
-    bench.simulate_data_loss();
+    b.simulate_data_loss();
     auto t2 = clock::now();
-    rc |= bench.decode();
+    rc |= b.decode();
     auto t3 = clock::now();
     if (rc != 0 && r.err_msg.empty()) r.err_msg = "Codec Failure";
-    if (!bench.check_for_corruption() && r.err_msg.empty()) r.err_msg = "Corruption Detected";
+    if (!b.check_for_corruption() && r.err_msg.empty()) r.err_msg = "Corruption Detected";
     enc.push_back(std::chrono::duration<double, std::nano>(t1 - t0).count());
     dec.push_back(std::chrono::duration<double, std::nano>(t3 - t2).count());
     ++r.iterations;
@@ -93,7 +96,7 @@ inline void write_csv_header(std::ostream& os) {
         "decode_throughput_Gbps_stddev\n";
 }
 
-inline void write_csv_row(std::ostream& os, const RunResult& r, const BenchmarkConfig& c) {
+inline void write_csv_row(std::ostream& os, const RunResult& r, const ::BenchmarkConfig& c) {
   os << '"' << r.name << "\"," << r.err_msg << ',' << r.iterations << ','
      << c.num_warmup_iterations << ',' << (c.gpu_computation ? 1 : 0) << ',' << c.num_gpu_blocks
      << ',' << c.threads_per_gpu_block << ',' << c.message_size << ',' << c.block_size << ",\"("

@@ -35,9 +35,17 @@
 //   --device D       HIP device of xorec-hip (default 0)
 //   --devices LIST   devices of xorec-hip-multi, comma separated, repeats allowed
 //                    (default: every visible device)
-//   --seed S         seed of payloads and erasure draws (the reference uses the clock)
+//   --seed S         seed of payloads (written on the device) and erasure draws
+//                    (default 0; XecPluginOptions::seeded)
 //   --sync MODE      hipSetDeviceFlags: 0 default, 1 spin, 2 yield, 3 blocking
-//   --host-validation  payload written/checked on the host + copies, as the reference
+//   --host-validation  the reference's own way: payloads from its wall-clock
+//                    write_validation_pattern on the host + one copy, erasures from
+//                    its select_lost_blocks, the check on the host after a copy back
+//                    (--seed is then unused)
+// The plugins are integration/xorec_hip_bm.cpp / xorec_hip_multi_bm.cpp -- the
+// drop-in sources themselves -- over this repo's restatement of the reference's
+// interface (integration/iface/); options beyond BenchmarkConfig travel in
+// XecPluginOptions.
 //   --stdout         CSV to stdout instead of -f
 //   --raw-dir DIR    directory for a bare -f name (default ../results/raw/; created
 //                    if missing; "" = the working directory)
@@ -57,6 +65,7 @@
 #include <vector>
 
 #include "runner.hpp"
+#include "xec_plugin_options.hpp"
 #include "xorec_hip_bm.hpp"
 #include "xorec_hip_multi_bm.hpp"
 
@@ -114,17 +123,21 @@ void usage() {
 }
 
 // get_gpu_configs (benchmark_suite.cpp:252-277), same loop order
-std::vector<xec::BenchmarkConfig> gpu_sweep(const xec::BenchmarkConfig& base) {
-  std::vector<xec::BenchmarkConfig> out;
-  for (size_t bs : xec::kVarBlockSizes)
-    for (const auto& ec : xec::kVarEcParams) {
+size_t parity_blocks(const BenchmarkConfig& c) {
+  return std::get<0>(c.ec_params) - std::get<1>(c.ec_params);
+}
+
+std::vector<BenchmarkConfig> gpu_sweep(const BenchmarkConfig& base) {
+  std::vector<BenchmarkConfig> out;
+  for (size_t bs : VAR_BLOCK_SIZES)
+    for (const auto& ec : VAR_EC_PARAMS) {
       const size_t m = std::get<0>(ec) - std::get<1>(ec);
-      for (size_t lost : xec::kVarNumLostBlocks) {
+      for (size_t lost : VAR_NUM_LOST_BLOCKS) {
         if (lost > m) continue;
-        for (size_t gb : xec::kVarNumGpuBlocks)
-          for (size_t tpb : xec::kVarNumThreadsPerBlock) {
-            xec::BenchmarkConfig c = base;
-            c.message_size = xec::kMessageSize;
+        for (size_t gb : VAR_NUM_GPU_BLOCKS)
+          for (size_t tpb : VAR_NUM_THREADS_PER_BLOCK) {
+            BenchmarkConfig c = base;
+            c.message_size = MESSAGE_SIZE;
             c.block_size = bs;
             c.ec_params = ec;
             c.num_lost_blocks = lost;
@@ -169,16 +182,18 @@ int main(int argc, char** argv) {
       {"raw-dir", required_argument, nullptr, kRawDir},
       {nullptr, 0, nullptr, 0}};
 
-  xec::BenchmarkConfig base;
+  BenchmarkConfig base{};
   base.num_iterations = 10;        // NUM_ITERATIONS (benchmark_suite.cpp:30)
   base.num_warmup_iterations = 0;  // NUM_WARMUP_ITERATIONS (:31)
   base.gpu_computation = true;
-  base.num_gpu_blocks = xec::kVarNumGpuBlocks[0];
-  base.threads_per_gpu_block = xec::kVarNumThreadsPerBlock[0];
+  base.num_gpu_blocks = VAR_NUM_GPU_BLOCKS[0];
+  base.threads_per_gpu_block = VAR_NUM_THREADS_PER_BLOCK[0];
   base.num_cpu_threads = static_cast<size_t>(omp_get_max_threads());
+  XecPluginOptions opt;
+  opt.seeded = true;  // reproducible unless --host-validation asks for the reference's clock
   // single-config defaults: BASELINE.json configs[2] (k=16+1, 1 MiB blocks,
   // 256 stripes = 4 GiB message, 1 lost block per stripe)
-  xec::BenchmarkConfig single = base;
+  BenchmarkConfig single = base;
   size_t k = 16, m = 1;
   single.block_size = 1u << 20;
   single.message_size = 256ull * 16 * (1u << 20);
@@ -228,19 +243,19 @@ int main(int argc, char** argv) {
       case kLost: single.num_lost_blocks = parse_size(optarg); single_mode = true; break;
       case kSweep: sweep = optarg; break;
       case kThreads: base.num_cpu_threads = parse_size(optarg); break;
-      case kDevice: base.device_id = std::atoi(optarg); break;
-      case kSeed: base.seed = parse_size(optarg); break;
-      case kSync: base.sync_mode = std::atoi(optarg); break;
-      case kHostVal: base.host_validation = true; break;
+      case kDevice: opt.device = std::atoi(optarg); break;
+      case kSeed: opt.seed = parse_size(optarg); break;
+      case kSync: opt.sync_mode = std::atoi(optarg); break;
+      case kHostVal: opt.seeded = false; opt.host_check = true; break;
       case kStdout: to_stdout = true; break;
       case kRawDir: raw_dir = optarg; break;
       case kDevices:
-        base.devices.clear();
+        opt.devices.clear();
         for (const auto& d : arg_vector(optarg)) {
           char* end = nullptr;
           const long v = std::strtol(d.c_str(), &end, 10);
           if (d.empty() || *end != '\0' || v < 0) fail("Invalid device: " + d);
-          base.devices.push_back(static_cast<int>(v));
+          opt.devices.push_back(static_cast<int>(v));
         }
         break;
       default: usage(); return EXIT_FAILURE;
@@ -249,15 +264,10 @@ int main(int argc, char** argv) {
   if (algorithms.empty())
     fail("No benchmarks selected. Use --gpu xorec-hip (or xorec-hip-multi) to select one.");
 
-  std::vector<xec::BenchmarkConfig> cfgs;
-  auto with_base = [&](xec::BenchmarkConfig x) {
+  std::vector<BenchmarkConfig> cfgs;
+  auto with_base = [&](BenchmarkConfig x) {
     x.num_iterations = base.num_iterations;
     x.num_warmup_iterations = base.num_warmup_iterations;
-    x.device_id = base.device_id;
-    x.seed = base.seed;
-    x.sync_mode = base.sync_mode;
-    x.host_validation = base.host_validation;
-    x.devices = base.devices;
     return x;
   };
   if (!sweep.empty()) {
@@ -268,7 +278,7 @@ int main(int argc, char** argv) {
       if (line.empty() || line[0] == '#') continue;
       unsigned long long ms, b, kk, mm, l;
       if (std::sscanf(line.c_str(), "%llu %llu %llu %llu %llu", &ms, &b, &kk, &mm, &l) != 5) continue;
-      xec::BenchmarkConfig x = with_base(base);
+      BenchmarkConfig x = with_base(base);
       x.message_size = ms;
       x.block_size = b;
       x.ec_params = {kk + mm, kk};
@@ -282,10 +292,10 @@ int main(int argc, char** argv) {
     cfgs = gpu_sweep(base);
   }
   for (const auto& x : cfgs) {
-    if (x.num_lost_blocks > xec::parity_blocks(x)) {
+    if (x.num_lost_blocks > parity_blocks(x)) {
       // the reference prints and exits (utils.cpp:102-105)
       std::fprintf(stderr, "lost blocks per stripe (%zu) must be <= parity blocks (%zu)\n",
-                   x.num_lost_blocks, xec::parity_blocks(x));
+                   x.num_lost_blocks, parity_blocks(x));
       return 2;
     }
   }
@@ -311,8 +321,8 @@ int main(int argc, char** argv) {
     for (const auto& alg : algorithms) {
       const bool multi = alg == "xorec-hip-multi";
       for (const auto& x : cfgs) {
-        xec::RunResult r = multi ? xec::run_generic<xec::XorecBenchmarkHipMulti>(kNameMulti, x)
-                                 : xec::run_generic<xec::XorecBenchmarkHip>(kName, x);
+        xec::RunResult r = multi ? xec::run_generic<XorecBenchmarkHipMulti>(kNameMulti, x, opt)
+                                 : xec::run_generic<XorecBenchmarkHip>(kName, x, opt);
         xec::write_csv_row(*os, r, x);
         os->flush();
         std::fprintf(stderr,

@@ -1,7 +1,8 @@
 // xec_multi_leg.cpp -- bench.py's "multi_device" leg: config 5 (BASELINE.json
 // configs[4]: k=16+1, 1 MiB shards, stripe batches partitioned over the GPUs of
 // one node) through the ONE-process multi-device plugin, XorecBenchmarkHipMulti
-// (host/xorec_hip_multi_bm.hpp), the form that fits the reference's single-
+// (integration/xorec_hip_multi_bm.hpp, the drop-in source itself), the form
+// that fits the reference's single-
 // process benchmark binary.  bench.py's headline runs one process per GPU;
 // this leg covers the plugin's own cross-device paths in the same run:
 //
@@ -38,6 +39,7 @@
 #include <vector>
 
 #include "xec.h"
+#include "xec_plugin_options.hpp"
 #include "xorec_hip_multi_bm.hpp"
 
 namespace {
@@ -84,20 +86,7 @@ std::string jnum(double v, int prec = 4) {
   return b;
 }
 
-// The plugin with the two read-only views the leg needs: the data blocks the
-// current erasure draw lost (decode's algorithmic bytes) -- protected
-// base-class state, no change to the plugin's interface.
-class LegBench : public xec::XorecBenchmarkHipMulti {
- public:
-  using XorecBenchmarkHipMulti::XorecBenchmarkHipMulti;
-  size_t lost_data_blocks() const {
-    size_t n = 0;
-    const uint8_t* bm = m_block_bitmap.get();
-    for (size_t c = 0; c < m_chunks; ++c)
-      for (size_t i = 0; i < m_chunk_data_blocks; ++i) n += bm[c * m_chunk_tot_blocks + i] == 0;
-    return n;
-  }
-};
+using LegBench = XorecBenchmarkHipMulti;
 
 struct Args {
   std::vector<int> devices;
@@ -192,7 +181,7 @@ bool exchange(LegBench& bench, const Args& a, size_t S_total, std::string& js) {
   release();
   // stripes that cross a link: every shard's range except the root's own
   size_t remote = 0;
-  for (size_t i = 0; i < bench.shards(); ++i)
+  for (size_t i = 0; i < bench.num_shards(); ++i)
     if (bench.shard_device(i) != a.root) remote += bench.shard_count(i);
   const double sc = t_sc.empty() ? 0 : *std::min_element(t_sc.begin(), t_sc.end());
   const double ga = t_ga.empty() ? 0 : *std::min_element(t_ga.begin(), t_ga.end());
@@ -238,7 +227,7 @@ int main(int argc, char** argv) {
   js += ",\"distinct_devices\":" + std::to_string(distinct);
   bool pass = false;
   try {
-    xec::BenchmarkConfig c;
+    BenchmarkConfig c{};
     c.message_size = S_total * a.k * a.bs;
     c.block_size = a.bs;
     c.ec_params = {a.k + a.m, a.k};
@@ -246,10 +235,13 @@ int main(int argc, char** argv) {
     c.num_cpu_threads = 1;
     c.num_iterations = a.iters;
     c.num_warmup_iterations = a.warmup;
-    c.seed = kSeed;
-    c.devices = a.devices;
+    c.gpu_computation = true;
+    XecPluginOptions opt;
+    opt.seeded = true;  // device payloads: a 32 GiB batch at 8 GPUs
+    opt.seed = kSeed;
+    opt.devices = a.devices;
     const double t_init = now_s();
-    LegBench bench(c);
+    LegBench bench(c, opt);
     // PCI bus of each device and peer access to the root (xGMI where 1)
     js += ",\"pci_bus_ids\":[";
     for (size_t i = 0; i < n; ++i) {

@@ -9,8 +9,8 @@ from .codec import (DECODE_KERNELS, Pipeline, build_info, check_args, check_bitm
                     decode_device, decode_device_list, decode_per_stripe, decode_tiling_used,
                     device_list_bytes, encode, erase,
                     fill_splitmix64, init,
-                    set_decode_tiling, set_launch, set_occupancy, set_rotation,
-                    set_validate_kernel,
+                    select_lost_blocks, set_decode_tiling, set_launch, set_occupancy,
+                    set_rotation, set_validate_kernel,
                     status_string, validate_blocks, write_validation_pattern)
 from .partition import stripe_range
 
@@ -18,7 +18,8 @@ __all__ = [
     "DECODE_KERNELS", "EXPORTED", "LIB_PATH", "Pipeline", "Status", "XecLibraryError", "lib",
     "build_info", "check_args", "check_bitmap", "decode", "decode_device", "decode_device_list",
     "decode_per_stripe", "decode_tiling_used", "device_list_bytes",
-    "encode", "erase", "fill_splitmix64", "init", "set_decode_tiling", "set_launch",
+    "encode", "erase", "fill_splitmix64", "init", "select_lost_blocks", "set_decode_tiling",
+    "set_launch",
     "set_occupancy", "set_rotation", "set_validate_kernel", "status_string", "stripe_range", "validate_blocks",
     "write_validation_pattern",
 ]

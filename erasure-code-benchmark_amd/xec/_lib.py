@@ -28,7 +28,7 @@ EXPORTED = (
     "xec_decode_device", "xec_set_occupancy", "xec_set_decode_tiling",
     "xec_set_validate_kernel", "xec_decode_tiling_used", "xec_decode_per_stripe",
     "xec_decode_device_list", "xec_decode_device_list_bytes", "xec_get_tuning",
-    "xec_set_tuning", "xec_set_rotation",
+    "xec_set_tuning", "xec_set_rotation", "xec_select_lost_blocks",
 )
 
 
@@ -107,6 +107,7 @@ def lib() -> ctypes.CDLL:
         "xec_set_rotation": ([ctypes.c_int], st),
         "xec_get_tuning": ([ctypes.POINTER(Tuning)], st),
         "xec_set_tuning": ([ctypes.POINTER(Tuning)], st),
+        "xec_select_lost_blocks": ([sz, sz, sz, vp, ctypes.c_uint64], st),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -112,6 +112,12 @@ def check_bitmap(h_bitmap, S: int, k: int, m: int) -> tuple[Status, bool]:
     return st, bool(needs.value)
 
 
+def select_lost_blocks(k: int, m: int, lost: int, h_bitmap, seed: int) -> Status:
+    """xec_select_lost_blocks -- utils.cpp:100-127 with an explicit seed, on one
+    stripe's (k+m)-byte host bitmap (host only)."""
+    return Status(lib().xec_select_lost_blocks(k, m, lost, _ptr(h_bitmap), seed))
+
+
 def check_args(data_addr: int, parity_addr: int, bs: int, k: int, m: int) -> Status:
     """Host-only xorec_check_args (xorec_utils.hpp:61-86)."""
     return Status(lib().xec_check_args(data_addr, parity_addr, bs, k, m))

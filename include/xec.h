@@ -180,6 +180,16 @@ xec_status xec_check_args(const void* data, const void* parity, size_t bs, size_
 xec_status xec_erase(void* d_data, void* d_parity, size_t S, size_t bs, size_t k, size_t m,
                      const uint8_t* d_bitmap, hipStream_t stream);
 
+/* Host-only erasure draw for one stripe's (k+m)-byte bitmap: the reference's
+ * select_lost_blocks (src/utils/utils.cpp:100-127) with an explicit seed in
+ * place of its wall clock -- `lost` draws from PCG32(RANDOM_SEED + seed,
+ * stream 1) over the blocks still eligible, each draw marking its block 0 and
+ * removing its parity class, so the set is always recoverable.  lost == 0
+ * leaves the bitmap as it is; lost > m is XEC_INVALID_COUNTS (where the
+ * reference prints and exits). */
+xec_status xec_select_lost_blocks(size_t k, size_t m, size_t lost, uint8_t* h_bitmap,
+                                  uint64_t seed);
+
 /* Synthetic input generator (tests and bench): stripe c's stripe_bytes are
  * little-endian u64 splitmix64 outputs from state seed_base + c.
  * stripe_bytes % 8 == 0 and d_buf 8-B aligned, else XEC_INVALID_SIZE /

@@ -12,7 +12,8 @@ uint8_t* alloc_device(size_t bytes) {
 
 uint8_t* alloc_pinned(size_t bytes) {
   void* p = nullptr;
-  return hipHostMalloc(&p, bytes ? bytes : 64, hipHostMallocDefault) == hipSuccess
+  // portable: every device of the process may read it (XorecBenchmarkHipMulti)
+  return hipHostMalloc(&p, bytes ? bytes : 64, hipHostMallocPortable) == hipSuccess
              ? static_cast<uint8_t*>(p)
              : nullptr;
 }
@@ -55,6 +56,17 @@ int current_device() {
 }
 
 bool set_device(int device) { return hipSetDevice(device) == hipSuccess; }
+
+bool set_sync_mode(int mode) {
+  static const unsigned flags[] = {0, hipDeviceScheduleSpin, hipDeviceScheduleYield,
+                                   hipDeviceScheduleBlockingSync};
+  if (mode <= 0 || mode > 3) return mode == 0;
+  // only possible before the device's context is active: a later call is
+  // refused by the runtime, and its error is this call's to clear
+  if (hipSetDeviceFlags(flags[mode]) == hipSuccess) return true;
+  (void)hipGetLastError();
+  return false;
+}
 
 bool enable_peer_access(int device, int peer) {
   if (device == peer) return true;

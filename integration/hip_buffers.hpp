@@ -40,6 +40,11 @@ int device_count();
 int current_device();
 bool set_device(int device);
 
+// hipSetDeviceFlags for the current device: 0 leaves the runtime default, 1
+// spin, 2 yield, 3 blocking sync; false if the runtime refused (a context
+// already active).
+bool set_sync_mode(int mode);
+
 // `device` gets access to `peer`'s memory where the pair supports it (an
 // access already enabled is fine); true unless a runtime call failed.
 bool enable_peer_access(int device, int peer);

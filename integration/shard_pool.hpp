@@ -1,4 +1,5 @@
-// shard_pool.hpp -- one worker thread per device shard of XorecBenchmarkHipMulti.
+// shard_pool.hpp -- one worker thread per device shard of XorecBenchmarkHipMulti
+// (plain C++, no reference or HIP header: compiled into the plugin in both builds).
 //
 // run(fn) calls fn(i) for every shard i at once -- shard 0 on the calling
 // thread, shard i > 0 on worker i -- and returns when all calls have.  Used
@@ -17,21 +18,23 @@
 #include <thread>
 #include <vector>
 
-namespace xec {
+namespace xec_hip {
 
 class ShardPool {
  public:
+  // A thread that cannot be started leaves none running: the ones already
+  // started are stopped and joined before the exception leaves (a throwing
+  // constructor runs no destructor, and a joinable std::thread would
+  // terminate the process).
   explicit ShardPool(size_t shards) : n_(shards) {
-    for (size_t i = 1; i < n_; ++i) threads_.emplace_back([this, i] { worker(i); });
-  }
-  ~ShardPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
+    try {
+      for (size_t i = 1; i < n_; ++i) threads_.emplace_back([this, i] { worker(i); });
+    } catch (...) {
+      stop_all();
+      throw;
     }
-    go_.notify_all();
-    for (std::thread& t : threads_) t.join();
   }
+  ~ShardPool() { stop_all(); }
   ShardPool(const ShardPool&) = delete;
   ShardPool& operator=(const ShardPool&) = delete;
 
@@ -54,6 +57,16 @@ class ShardPool {
   }
 
  private:
+  void stop_all() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    go_.notify_all();
+    for (std::thread& t : threads_) t.join();
+    threads_.clear();
+  }
+
   void worker(size_t i) {
     uint64_t seen = 0;
     std::unique_lock<std::mutex> lk(mu_);
@@ -104,4 +117,4 @@ class Rendezvous {
   std::condition_variable cv_;
 };
 
-}  // namespace xec
+}  // namespace xec_hip

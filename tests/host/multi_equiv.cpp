@@ -30,13 +30,13 @@ void spoil(uint8_t* bm, size_t c, size_t k, size_t m) {
     }
 }
 
-class Multi : public xec::XorecBenchmarkHipMulti {
+class Multi : public XorecBenchmarkHipMulti {
  public:
   using XorecBenchmarkHipMulti::XorecBenchmarkHipMulti;
   void spoil_stripe(size_t c) { spoil(m_block_bitmap.get(), c, m_chunk_data_blocks, m_chunk_parity_blocks); }
 };
 
-class Single : public xec::XorecBenchmarkHip {
+class Single : public XorecBenchmarkHip {
  public:
   using XorecBenchmarkHip::XorecBenchmarkHip;
   void spoil_stripe(size_t c) { spoil(m_block_bitmap.get(), c, m_chunk_data_blocks, m_chunk_parity_blocks); }
@@ -49,28 +49,31 @@ class Single : public xec::XorecBenchmarkHip {
   }
 };
 
-void read_multi(const xec::XorecBenchmarkHipMulti& b, size_t kbs, size_t mbs,
+void read_multi(const XorecBenchmarkHipMulti& b, size_t kbs, size_t mbs,
                 std::vector<uint8_t>& d, std::vector<uint8_t>& p, size_t S) {
   d.assign(S * kbs, 0);
   p.assign(S * mbs, 0);
-  for (size_t i = 0; i < b.shards(); ++i)
+  for (size_t i = 0; i < b.num_shards(); ++i)
     if (!b.read_shard(i, d.data() + b.shard_first(i) * kbs, p.data() + b.shard_first(i) * mbs))
       std::fprintf(stderr, "read_shard %zu failed\n", i);
 }
 
 int check(size_t S, size_t k, size_t m, size_t bs, size_t lost, std::vector<int> devices,
           bool unrecoverable = false) {
-  xec::BenchmarkConfig c;
+  BenchmarkConfig c{};
   c.message_size = S * k * bs;
   c.block_size = bs;
   c.ec_params = {k + m, k};
   c.num_lost_blocks = lost;
   c.num_cpu_threads = 4;
-  c.seed = 5;
-  c.devices = devices;
-  Single one(c);
-  Multi multi(c);
-  if (multi.shards() != devices.size()) return 10;
+  c.gpu_computation = true;
+  XecPluginOptions opt;
+  opt.seeded = true;
+  opt.seed = 5;
+  opt.devices = devices;
+  Single one(c, opt);
+  Multi multi(c, opt);
+  if (multi.num_shards() != devices.size()) return 10;
   std::vector<uint8_t> d1, p1, dn, pn;
   int step = 0;
   auto same = [&](bool parity) {

@@ -27,15 +27,18 @@ double now() {
 }
 
 int check(size_t S, size_t k, size_t m, size_t bs, std::vector<int> devices) {
-  xec::BenchmarkConfig c;
+  BenchmarkConfig c{};
   c.message_size = S * k * bs;
   c.block_size = bs;
   c.ec_params = {k + m, k};
   c.num_lost_blocks = 0;
   c.num_cpu_threads = 4;
-  c.seed = 11;
-  c.devices = devices;
-  xec::XorecBenchmarkHipMulti multi(c);
+  c.gpu_computation = true;
+  XecPluginOptions opt;
+  opt.seeded = true;
+  opt.seed = 11;
+  opt.devices = devices;
+  XorecBenchmarkHipMulti multi(c, opt);
   if (hipSetDevice(0) != hipSuccess) return 20;
   uint8_t *root = nullptr, *root_par = nullptr, *ref_par = nullptr;
   if (hipMalloc(&root, S * k * bs) != hipSuccess || hipMalloc(&root_par, S * m * bs) != hipSuccess ||
@@ -66,7 +69,7 @@ int check(size_t S, size_t k, size_t m, size_t bs, std::vector<int> devices) {
                   hipMemcpy(hd.data(), root, hd.size(), hipMemcpyDeviceToHost) != hipSuccess))
     rc = 23;
   if (rc == 0 && a != b) rc = 4;  // gathered parity == root's own encode
-  for (size_t i = 0; rc == 0 && i < multi.shards(); ++i) {
+  for (size_t i = 0; rc == 0 && i < multi.num_shards(); ++i) {
     const size_t f = multi.shard_first(i), n = multi.shard_count(i);
     if (!multi.read_shard(i, sd.data(), sp.data())) rc = 24;
     else if (std::memcmp(sd.data(), hd.data() + f * k * bs, n * k * bs) != 0) rc = 5;

@@ -1,7 +1,7 @@
 // plugin_defaults.cpp -- a CPU plugin that overrides ONLY setup / encode /
 // decode, run through the harness loop (host/runner.hpp): the base class's
 // default simulate_data_loss, check_for_corruption and m_write_data_buffer
-// (host/abstract_bm.cpp, restating abstract_bm.cpp:20-61) must make it work,
+// (integration/iface/abstract_bm.cpp, restating abstract_bm.cpp:20-60) must make it work,
 // as the reference's CPU plugins rely on (e.g. xorec_bm.cpp:6-58).  The codec
 // here is the oracle's C restatement (test infrastructure).  A second plugin
 // whose decode does nothing must be caught by the default corruption check.
@@ -14,11 +14,11 @@
 
 namespace {
 
-class CpuXorecPlugin : public xec::AbstractBenchmark {
+class CpuXorecPlugin : public AbstractBenchmark {
  public:
-  explicit CpuXorecPlugin(const xec::BenchmarkConfig& c) : AbstractBenchmark(c) {}
+  explicit CpuXorecPlugin(const BenchmarkConfig& c, const XecPluginOptions& = {})
+      : AbstractBenchmark(c) {}
   void setup() noexcept override {
-    ++m_round;
     std::memset(m_block_bitmap.get(), 1, m_chunks * m_chunk_tot_blocks);
     m_write_data_buffer();
   }
@@ -47,8 +47,8 @@ void expect(bool ok, const std::string& what) {
   }
 }
 
-xec::BenchmarkConfig cfg(size_t msg, size_t bs, size_t k, size_t m, size_t lost) {
-  xec::BenchmarkConfig c;
+BenchmarkConfig cfg(size_t msg, size_t bs, size_t k, size_t m, size_t lost) {
+  BenchmarkConfig c{};
   c.message_size = msg;
   c.block_size = bs;
   c.ec_params = {k + m, k};
@@ -56,7 +56,6 @@ xec::BenchmarkConfig cfg(size_t msg, size_t bs, size_t k, size_t m, size_t lost)
   c.num_iterations = 3;
   c.num_warmup_iterations = 1;
   c.gpu_computation = false;
-  c.seed = 7;
   return c;
 }
 
@@ -70,11 +69,11 @@ int main() {
     const auto c = cfg(s[0], s[1], s[2], s[3], s[4]);
     const std::string tag = std::to_string(s[2]) + "+" + std::to_string(s[3]) + " lost " +
                             std::to_string(s[4]);
-    auto r = xec::run_generic<CpuXorecPlugin>("cpu", c);
+    auto r = xec::run_generic<CpuXorecPlugin>("cpu", c, XecPluginOptions{});
     expect(r.err_msg.empty(), "defaults, " + tag + ": " + r.err_msg);
     expect(r.iterations == 3, "iterations, " + tag);
     if (s[4] > 0) {
-      auto bad = xec::run_generic<NoDecodePlugin>("nodecode", c);
+      auto bad = xec::run_generic<NoDecodePlugin>("nodecode", c, XecPluginOptions{});
       expect(bad.err_msg == "Corruption Detected", "default check catches a skipped decode, " + tag);
     }
   }

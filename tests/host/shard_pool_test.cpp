@@ -1,4 +1,4 @@
-// ThreadSanitizer test of host/shard_pool.hpp (the multi-device plugin's
+// ThreadSanitizer test of integration/shard_pool.hpp (the multi-device plugin's
 // per-shard decode threads): every run() calls fn(i) exactly once per shard,
 // concurrently, and returns only after all of them; many back-to-back runs,
 // pool sizes 1..9, construction and destruction with idle workers; and the
@@ -12,7 +12,7 @@
 
 int main() {
   for (size_t n = 1; n <= 9; ++n) {
-    xec::ShardPool pool(n);
+    xec_hip::ShardPool pool(n);
     std::vector<int> hits(n, 0);  // plain ints: TSan flags any unordered access
     for (int round = 0; round < 2000; ++round) {
       std::atomic<size_t> running{0};
@@ -32,10 +32,10 @@ int main() {
     }
   }
   for (size_t n = 1; n <= 9; ++n) {
-    xec::ShardPool pool(n);
+    xec_hip::ShardPool pool(n);
     for (int round = 0; round < 500; ++round) {
       const size_t bad = static_cast<size_t>(round) % (n + 3);  // >= n: nobody fails
-      xec::Rendezvous rv(n);
+      xec_hip::Rendezvous rv(n);
       std::vector<int> before(n, 0), verdict(n, -1);  // plain ints, as above
       std::atomic<size_t> arrived{0};
       pool.run([&](size_t i) {
@@ -52,7 +52,7 @@ int main() {
         }
     }
   }
-  { xec::ShardPool idle(4); }  // destroyed without a run
+  { xec_hip::ShardPool idle(4); }  // destroyed without a run
   std::printf("shard_pool ok\n");
   return 0;
 }

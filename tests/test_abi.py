@@ -247,3 +247,25 @@ int main(void) {
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert p.returncode == 0, (p.returncode, p.stderr)
     assert p.stdout.startswith("DecodeFailure xec-hip gfx950")
+
+
+def test_select_lost_blocks_matches_oracle(oracle):
+    """xec_select_lost_blocks (host only) == the oracle's restatement of the
+    reference's select_lost_blocks (utils.cpp:100-127) with the same seed, and
+    every draw is recoverable (at most one loss per parity class)."""
+    import numpy as np
+
+    import xorec_oracle as xo
+    for k, m in [(4, 1), (16, 1), (8, 4), (32, 8), (16, 16), (5, 5), (64, 2)]:
+        for lost in range(0, m + 1):
+            for seed in (0, 1, 7, 1896, 2**40 + 3):
+                got = np.ones(k + m, np.uint8)
+                assert xec.select_lost_blocks(k, m, lost, got, seed) == xec.Status.SUCCESS
+                want = np.ones(k + m, np.uint8)
+                assert xo.np_select_lost_blocks(k, m, lost, want, seed) == 0
+                assert (got == want).all(), (k, m, lost, seed)
+                zeros = np.flatnonzero(got == 0)
+                assert len(zeros) == lost and len(set(zeros % m)) == lost
+    bm = np.ones(5, np.uint8)
+    assert xec.select_lost_blocks(4, 1, 2, bm, 0) == xec.Status.INVALID_COUNTS
+    assert (bm == 1).all()

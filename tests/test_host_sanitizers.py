@@ -43,12 +43,12 @@ def test_oracle_asan_ubsan(tmp_path):
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 def test_shard_pool_tsan(tmp_path):
-    """The multi-device plugin's per-shard decode threads (host/shard_pool.hpp)
+    """The multi-device plugin's per-shard decode threads (integration/shard_pool.hpp)
     under ThreadSanitizer: each run calls every shard once and returns after
     all of them, over 2,000 runs per pool size."""
     exe = tmp_path / "shard_pool_test"
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
-                    f"-I{ROOT / 'erasure-code-benchmark_amd' / 'host'}",
+                    f"-I{ROOT / 'integration'}",
                     str(ROOT / "tests" / "host" / "shard_pool_test.cpp"), "-o", str(exe)],
                    check=True, capture_output=True)
     p = run_tsan([str(exe)], timeout=300)

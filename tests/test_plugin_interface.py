@@ -1,5 +1,5 @@
-"""The plugin interface's default behaviour (host/abstract_bm.{hpp,cpp},
-restating the reference's abstract_bm.hpp:53-67 and abstract_bm.cpp:20-61):
+"""The plugin interface's default behaviour (integration/iface/abstract_bm.{hpp,cpp},
+restating the reference's abstract_bm.hpp:18-88 and abstract_bm.cpp:4-60):
 a CPU plugin that overrides only setup / encode / decode runs clean through
 the harness loop, and the default corruption check catches a skipped decode.
 CPU only (g++), also under ASan/UBSan."""
@@ -13,6 +13,7 @@ import pytest
 from conftest import ROOT
 
 HOST = ROOT / "erasure-code-benchmark_amd" / "host"
+IFACE = ROOT / "integration" / "iface"
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
@@ -24,9 +25,10 @@ def test_plugin_defaults(tmp_path, sanitize):
                     str(ROOT / "oracle" / "xorec_oracle.c"), "-o", str(obj)], check=True)
     exe = tmp_path / "plugin_defaults"
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fopenmp", *san, f"-I{HOST}",
-                    f"-I{ROOT / 'oracle'}", str(ROOT / "tests" / "host" / "plugin_defaults.cpp"),
-                    str(HOST / "abstract_bm.cpp"), str(HOST / "ec_utils.cpp"), str(obj),
-                    "-o", str(exe)], check=True)
+                    f"-I{IFACE}", f"-I{ROOT / 'integration'}", f"-I{ROOT / 'oracle'}",
+                    str(ROOT / "tests" / "host" / "plugin_defaults.cpp"),
+                    str(IFACE / "abstract_bm.cpp"), str(IFACE / "utils.cpp"),
+                    str(IFACE / "bm_config.cpp"), str(obj), "-o", str(exe)], check=True)
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "plugin_defaults ok" in p.stdout
