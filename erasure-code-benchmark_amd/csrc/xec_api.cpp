@@ -130,17 +130,35 @@ constexpr size_t kMaxStaging = 64;
 std::mutex g_stage_mu;
 std::vector<Staging*> g_stage;
 
+// The thread's pending HIP error and the library.  What
+// the runtime does (tools/lab/last_error_probe.hip, profiles/r05b): a call
+// that succeeds leaves a pending error alone; a call that fails replaces it;
+// hipErrorNotReady from a stream or event query is not recorded on ROCm 7.2,
+// but was read back as a launch failure under an earlier runtime
+// (profiles/r04s).  So the library (1) asks no query at all while an error of
+// the caller's is pending -- it takes the answer that needs none, which is
+// always correct -- (2) clears a NotReady only if that is what the query left
+// pending, and (3) reports any other query error as the call's failure,
+// leaving it pending for the caller.
+bool caller_error_pending() { return hipPeekAtLastError() != hipSuccess; }
+
+void clear_own_not_ready() {
+  if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
+}
+
 // hipEventQuery on a buffer's event (recorded on a stream the library owns,
-// track_stream below): true once the work it marks has passed.  The event is
-// the library's, so whatever its query raises -- hipErrorNotReady, "not yet",
-// or anything else, which keeps the buffer counted as in use -- is cleared,
-// unless an error of the caller's was already pending (then nothing is
-// touched).
-bool event_passed(hipEvent_t e) {
-  const bool clean = hipPeekAtLastError() == hipSuccess;
+// track_stream below): 1 once the work it marks has passed, 0 not yet (or not
+// asked: a caller's error is pending, and the buffer is taken as in use), -1
+// the query failed -- a sticky device fault, which fails the call.
+int event_passed(hipEvent_t e) {
+  if (caller_error_pending()) return 0;
   const hipError_t q = hipEventQuery(e);
-  if (q != hipSuccess && clean) (void)hipGetLastError();
-  return q == hipSuccess;
+  if (q == hipSuccess) return 1;
+  if (q == hipErrorNotReady) {
+    clear_own_not_ready();
+    return 0;
+  }
+  return -1;
 }
 
 // A buffer read by the caller's stream is free once that stream has passed
@@ -148,26 +166,43 @@ bool event_passed(hipEvent_t e) {
 // that stream (a pipeline destroys its streams), and querying it later made
 // HIP report a stray error (hipErrorStreamCaptureUnsupported, read by the
 // next launch's hipGetLastError: tools/fuzz_big.py --pipeline, profiles/r04s).
-// So the caller's stream only hands over to a per-device tracking stream of
-// the library's (hipStreamWaitEvent on a throw-away record), and the buffer's
-// event is recorded there (g_track_mu guards the stream list).
+// So the caller's stream only hands over to a tracking stream of the
+// library's (hipStreamWaitEvent on a throw-away record), and the buffer's
+// event is recorded there.  A tracking stream waits for its callers in the
+// order the hand-offs were queued, so one shared stream would keep a short
+// decode's buffer busy behind every earlier caller's unrelated long work
+// (ADVICE r04): each device has kTrackLanes of them, a caller stream always
+// hands over to the same lane (its handle hashed), so independent callers on
+// different streams rarely share one (g_track_mu guards the list).
+constexpr size_t kTrackLanes = 4;
 std::mutex g_track_mu;
-std::vector<std::pair<int, hipStream_t>> g_track_streams;
-hipStream_t track_stream(int dev) {
+struct TrackLanes {
+  int dev;
+  hipStream_t lane[kTrackLanes];
+};
+std::vector<TrackLanes> g_track_streams;
+hipStream_t track_stream(int dev, hipStream_t caller) {
+  const uintptr_t h = reinterpret_cast<uintptr_t>(caller);
+  const size_t lane = static_cast<size_t>((h >> 4) ^ (h >> 12)) % kTrackLanes;
   std::lock_guard<std::mutex> lk(g_track_mu);
   for (auto& ts : g_track_streams)
-    if (ts.first == dev) return ts.second;
-  hipStream_t s = nullptr;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  g_track_streams.emplace_back(dev, s);
-  return s;
+    if (ts.dev == dev) return ts.lane[lane];
+  TrackLanes t{dev, {}};
+  for (auto& s : t.lane)
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      for (auto& made : t.lane)
+        if (made != nullptr) (void)hipStreamDestroy(made);
+      return nullptr;
+    }
+  g_track_streams.push_back(t);
+  return t.lane[lane];
 }
 
-// Record `done` once `caller` has passed its current work, on the library's
-// tracking stream of `dev` (`handoff` is the throw-away record on the caller's
+// Record `done` once `caller` has passed its current work, on a tracking
+// stream of `dev` (`handoff` is the throw-away record on the caller's
 // stream); false if that cannot be queued.
 bool record_after(hipEvent_t done, hipEvent_t handoff, hipStream_t caller, int dev) {
-  const hipStream_t ts = track_stream(dev);
+  const hipStream_t ts = track_stream(dev, caller);
   return ts != nullptr && hipEventRecord(handoff, caller) == hipSuccess &&
          hipStreamWaitEvent(ts, handoff, 0) == hipSuccess && hipEventRecord(done, ts) == hipSuccess;
 }
@@ -175,14 +210,21 @@ bool record_after(hipEvent_t done, hipEvent_t handoff, hipStream_t caller, int d
 // The slot is picked and marked busy under the lock; waiting for a recycled
 // buffer's last reader and re-allocating happen after the lock is dropped, so
 // one thread waiting for another's copy never stalls other threads' calls.
-Staging* stage_acquire(size_t bytes, int dev) {
+// *fault: an event query failed (event_passed -1); nullptr is returned and
+// the call must fail.
+Staging* stage_acquire(size_t bytes, int dev, bool* fault) {
   Staging* pick = nullptr;
   bool recycled = false;
   {
     std::lock_guard<std::mutex> lk(g_stage_mu);
     for (Staging* st : g_stage) {
       if (st->busy || st->device != dev || st->cap < bytes) continue;
-      if (!event_passed(st->done)) continue;  // a queued copy still reads it
+      const int passed = event_passed(st->done);
+      if (passed < 0) {
+        *fault = true;
+        return nullptr;
+      }
+      if (passed == 0) continue;  // a queued copy still reads it
       if (pick == nullptr || st->cap < pick->cap) pick = st;
     }
     if (pick == nullptr && g_stage.size() >= kMaxStaging) {
@@ -212,7 +254,7 @@ Staging* stage_acquire(size_t bytes, int dev) {
     return nullptr;
   };
   if (recycled && hipEventSynchronize(pick->done) != hipSuccess) {
-    (void)hipGetLastError();  // the library's own event
+    *fault = true;  // a sticky fault: left pending for the caller
     return give_back();
   }
   if (pick->cap < bytes) {
@@ -305,9 +347,12 @@ bool side_uploads() {
 // refrows_ab.sh, profiles/r03zk).  A NotReady answer is cleared so that no
 // later hipGetLastError reads it as a launch failure; any other answer (a
 // sticky fault of earlier work, an invalid stream) is an error the caller
-// gets back as XEC_DEVICE_ERROR, and is left for its hipGetLastError.
+// gets back as XEC_DEVICE_ERROR, and is left for its hipGetLastError.  While
+// an error of the caller's is pending nothing is asked: the stream is taken as
+// idle (the copy goes on it, correct either way) and the error stays theirs.
 // Returns 0 idle, 1 busy, -1 error.
 int stream_busy(hipStream_t stream) {
+  if (caller_error_pending()) return 0;
   const hipError_t q = hipStreamQuery(stream);
   if (q == hipSuccess) return 0;
   if (q != hipErrorNotReady) {
@@ -315,7 +360,7 @@ int stream_busy(hipStream_t stream) {
       std::fprintf(stderr, "xec: hipStreamQuery: %s\n", hipGetErrorName(q));
     return -1;
   }
-  (void)hipGetLastError();
+  clear_own_not_ready();
   return 1;
 }
 
@@ -353,11 +398,12 @@ bool capturing(hipStream_t stream) {
 }
 
 // Starts copying `bytes` of host memory to a library buffer on the device's
-// copy stream; false (nothing queued) if no buffer or stream can be had.
+// copy stream; false (nothing queued) if no buffer or stream can be had, and
+// then *fault if an event query or wait failed (the call must fail).
 // `dev` is the current device (StreamDevice).  As in stage_acquire, a slot is
 // picked and marked busy under the lock, and a recycled slot's wait and
 // re-allocation happen outside it.
-bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
+bool upload_begin(const void* host, size_t bytes, int dev, Upload& up, bool* fault) {
   DevSlot* pick = nullptr;
   hipStream_t cs = nullptr;
   bool recycled = false;
@@ -367,7 +413,12 @@ bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
     if (cs == nullptr) return false;
     for (DevSlot* sl : g_slots) {
       if (sl->busy || sl->device != dev || sl->cap < bytes) continue;
-      if (!event_passed(sl->done)) continue;  // a kernel still reads it
+      const int passed = event_passed(sl->done);
+      if (passed < 0) {
+        *fault = true;
+        return false;
+      }
+      if (passed == 0) continue;  // a kernel still reads it
       if (pick == nullptr || sl->cap < pick->cap) pick = sl;
     }
     size_t mine = 0;
@@ -402,7 +453,7 @@ bool upload_begin(const void* host, size_t bytes, int dev, Upload& up) {
     return false;
   };
   if (recycled && hipEventSynchronize(pick->done) != hipSuccess) {
-    (void)hipGetLastError();  // the library's own event
+    *fault = true;  // a sticky fault: left pending for the caller
     return give_back();
   }
   if (pick->cap < bytes) {
@@ -650,7 +701,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   // on `stream`); for large bitmaps before the scan, so the two overlap.
   Upload bmu;
   auto upload_bitmap = [&]() -> bool {
-    if (side() && upload_begin(h_bitmap, bitmap_bytes, dev, bmu)) return true;
+    if (side() && upload_begin(h_bitmap, bitmap_bytes, dev, bmu, &query_failed)) return true;
     if (query_failed) return false;
     bmu = Upload{};
     bmu.dev = d_bitmap;
@@ -704,7 +755,11 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
       upload_end(bmu, stream, false);
       return DEVERR(hipSuccess);
     }
-    if (off_stream || n <= cap) sg = stage_acquire(n * 4, dev);
+    if (off_stream || n <= cap) sg = stage_acquire(n * 4, dev, &query_failed);
+    if (query_failed) {
+      upload_end(bmu, stream, false);
+      return DEVERR(hipSuccess);
+    }
     if (sg != nullptr) {
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, static_cast<uint32_t*>(sg->host), n);
       if (st != XEC_SUCCESS) {
@@ -714,9 +769,13 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
       }
       Upload lu;
       bool ok = true;
-      if (side() && upload_begin(sg->host, n * 4, dev, lu)) {
+      if (side() && upload_begin(sg->host, n * 4, dev, lu, &query_failed)) {
         stage_release(sg, true, lu.cs, true);
         ok = upload_join(lu, stream);
+      } else if (query_failed) {
+        stage_release(sg, false, stream, false);
+        upload_end(bmu, stream, false);
+        return DEVERR(hipSuccess);
       } else if (n <= cap) {
         // stream-ordered after any bitmap copy into the same scratch
         lu.dev = d_bitmap + pad;
@@ -811,20 +870,25 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
   const int dev = sd.device();
   const int busy = side_uploads() ? stream_busy(stream) : 0;
   if (busy < 0) return XEC_DEVICE_ERROR;
-  Staging* sg = stage_acquire(n * 4, dev);
+  bool fault = false;
+  Staging* sg = stage_acquire(n * 4, dev, &fault);
   if (sg == nullptr) return XEC_DEVICE_ERROR;
   uint32_t* items = static_cast<uint32_t*>(sg->host);
   (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, n, &n, &failures);
   rotate_for(items, n);
   g_tiling_used = XEC_TILING_LIST;
   Upload lu;
-  if (busy == 1 && upload_begin(items, n * 4, dev, lu)) {
+  if (busy == 1 && upload_begin(items, n * 4, dev, lu, &fault)) {
     stage_release(sg, true, lu.cs, true);
     const bool ok = upload_join(lu, stream) &&
                     xec::launch_decode(d_data, d_parity, lu.dev, g, ls, xec::kDecodeListTiles,
                                        stream, n) == hipSuccess;
     upload_end(lu, stream, true);
     return ok ? verdict : XEC_DEVICE_ERROR;
+  }
+  if (fault) {  // an event query or wait failed in upload_begin
+    stage_release(sg, false, stream, false);
+    return XEC_DEVICE_ERROR;
   }
   const size_t pad = (4 - reinterpret_cast<uintptr_t>(d_bitmap) % 4) % 4;
   const uint64_t cap = (S * (k + m) - pad) / 4;  // >= 511 here: n > 1,024 <= S*k

@@ -56,13 +56,29 @@ inline uint32_t grid_for(uint64_t work_items, uint32_t max_grid, uint32_t thread
   return (uint32_t)(grid ? grid : 1);
 }
 
-// The status of the launch(es) a wrapper just made: the error pending now,
-// unless it is the one already pending before them (`before`, an earlier
-// call's -- the caller's to read, so it is neither reported nor cleared here).
-inline hipError_t launch_status(hipError_t before) {
-  const hipError_t now = hipPeekAtLastError();
-  if (now == hipSuccess || now == before) return hipSuccess;
-  return hipGetLastError();
+// Test hook: XEC_TEST_FAIL_LAUNCH=1 in the environment (read once) makes every
+// kernel launch of the library invalid (2048 threads per workgroup), so that a
+// test sees the wrappers report a genuine launch failure while an error of the
+// caller's with the same code is pending (tests/host/error_preserve.cpp).
+bool fail_launch_for_test();
+
+template <typename T>
+struct NoDeduce {
+  using type = T;
+};
+
+// Launches `kernel` and returns THIS launch's status, from hipLaunchKernel
+// itself.  The thread's pending error is neither read nor cleared: one the
+// caller left unread stays theirs (a successful launch does not touch it,
+// tools/lab/last_error_probe.hip, profiles/r05b), and a failed launch is
+// reported whatever was pending before (comparing the pending
+// error before and after took a failure with the caller's code for success).
+template <typename... P>
+hipError_t launch(void (*kernel)(P...), dim3 grid, dim3 block, uint32_t lds, hipStream_t s,
+                  typename NoDeduce<P>::type... args) {
+  void* argv[] = {static_cast<void*>(&args)...};
+  if (fail_launch_for_test()) block = dim3(2048);
+  return hipLaunchKernel(reinterpret_cast<const void*>(kernel), grid, block, argv, lds, s);
 }
 
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,

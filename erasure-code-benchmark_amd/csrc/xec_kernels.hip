@@ -26,6 +26,7 @@
 // indices of xorec_gpu_cmp.cu:127-131).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 
 #include "xec_kernels.h"
@@ -471,35 +472,26 @@ namespace {
 template <int NM, int U, bool NT, int T>
 hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t grid,
                            uint32_t lds, hipStream_t s) {
-  const hipError_t before = hipPeekAtLastError();
-  encode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<const uint8_t*>(d),
-                                                 static_cast<uint8_t*>(p), g);
-  return launch_status(before);
+  return launch(encode_kernel<NM, U, NT, T>, grid, T, lds, s, static_cast<const uint8_t*>(d),
+                static_cast<uint8_t*>(p), g);
 }
 
 template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
                            int tiling, uint32_t grid, uint32_t lds, hipStream_t s,
                            const ArgItems* args) {
-  const hipError_t before = hipPeekAtLastError();
+  uint8_t* dd = static_cast<uint8_t*>(d);
+  const uint8_t* pp = static_cast<const uint8_t*>(p);
+  const uint32_t* list = reinterpret_cast<const uint32_t*>(bm);
   if (tiling == kDecodeDevListTiles)
-    decode_devlist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
-        static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p),
-        reinterpret_cast<const uint32_t*>(bm), g);
-  else if (tiling == kDecodeArgListTiles)
-    decode_arglist_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
-        static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p), g, *args);
-  else if (tiling == kDecodeListTiles)
-    decode_list_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(
-        static_cast<uint8_t*>(d), static_cast<const uint8_t*>(p),
-        reinterpret_cast<const uint32_t*>(bm), g);
-  else if (tiling == kDecodeClassTiles)
-    decode_class_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<uint8_t*>(d),
-                                                         static_cast<const uint8_t*>(p), bm, g);
-  else
-    decode_kernel<NM, U, NT, T><<<grid, T, lds, s>>>(static_cast<uint8_t*>(d),
-                                                   static_cast<const uint8_t*>(p), bm, g);
-  return launch_status(before);
+    return launch(decode_devlist_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
+  if (tiling == kDecodeArgListTiles)
+    return launch(decode_arglist_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, g, *args);
+  if (tiling == kDecodeListTiles)
+    return launch(decode_list_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
+  if (tiling == kDecodeClassTiles)
+    return launch(decode_class_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, bm, g);
+  return launch(decode_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, bm, g);
 }
 
 // Member counts (k/m) compiled fully unrolled: those of the reference's sweep
@@ -593,41 +585,42 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
 
 hipError_t launch_check(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
                         hipStream_t s) {
-  const hipError_t before = hipPeekAtLastError();
   const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
-  check_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status);
-  return launch_status(before);
+  return launch(check_kernel, grid, 256, 0, s, d_bitmap, g, d_status);
 }
 
 hipError_t launch_scan_list(const uint8_t* d_bitmap, const Geometry& g, int32_t* d_status,
                             uint32_t* d_list, hipStream_t s) {
-  const hipError_t before = hipPeekAtLastError();
-  reset_status_list_kernel<<<1, 1, 0, s>>>(d_status, d_list);
+  const hipError_t e = launch(reset_status_list_kernel, 1, 1, 0, s, d_status, d_list);
+  if (e != hipSuccess) return e;
   const uint32_t grid = grid_for((g.S * g.m + 255) / 256, 8192, 256);
-  scan_list_kernel<<<grid, 256, 0, s>>>(d_bitmap, g, d_status, d_list);
-  return launch_status(before);
+  return launch(scan_list_kernel, grid, 256, 0, s, d_bitmap, g, d_status, d_list);
 }
 
 hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, const Geometry& g,
                         hipStream_t s) {
-  const hipError_t before = hipPeekAtLastError();
   const uint64_t nblocks = g.S * (g.k + g.m);
   const uint32_t grid = grid_for(nblocks, 65536, 256);
-  erase_kernel<<<grid, 256, 0, s>>>(static_cast<uint8_t*>(d_data), static_cast<uint8_t*>(d_parity),
-                                    d_bitmap, g);
-  return launch_status(before);
+  return launch(erase_kernel, grid, 256, 0, s, static_cast<uint8_t*>(d_data),
+                static_cast<uint8_t*>(d_parity), d_bitmap, g);
 }
 
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,
                        hipStream_t s) {
-  const hipError_t before = hipPeekAtLastError();
   uint64_t gx = (words + 255) / 256;
   if (gx > 1024) gx = 1024;
   const uint64_t gy = S < 65535 ? S : 65535;
   if (gx == 0 || gy == 0) return hipSuccess;
-  fill_kernel<<<dim3((uint32_t)gx, (uint32_t)gy), 256, 0, s>>>(static_cast<uint64_t*>(d_buf), S,
-                                                              words, seed_base);
-  return launch_status(before);
+  return launch(fill_kernel, dim3((uint32_t)gx, (uint32_t)gy), 256, 0, s,
+                static_cast<uint64_t*>(d_buf), S, words, seed_base);
+}
+
+bool fail_launch_for_test() {
+  static const bool on = [] {
+    const char* e = std::getenv("XEC_TEST_FAIL_LAUNCH");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
 }
 
 // Loads this file's code object onto the current device (see xec_kernels.h).

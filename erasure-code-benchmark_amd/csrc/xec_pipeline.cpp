@@ -129,18 +129,20 @@ class HostCopier {
 class HostPool {
  public:
   using Piece = HostCopier::Piece;
+  // A thread that cannot be started leaves none behind: the ones already
+  // running are stopped and joined before the exception leaves the
+  // constructor (no destructor runs then, and a joinable std::thread would
+  // terminate the process instead of reaching ensure_stage's catch).
   HostPool(int device, unsigned threads, size_t jobs)
       : device_(device), left_(jobs, 0), failed_(jobs, 0) {
-    for (unsigned t = 0; t < threads; ++t) th_.emplace_back([this] { run(); });
-  }
-  ~HostPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
+    try {
+      for (unsigned t = 0; t < threads; ++t) th_.emplace_back([this] { run(); });
+    } catch (...) {
+      stop_all();
+      throw;
     }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();  // the queue is drained first
   }
+  ~HostPool() { stop_all(); }
   // Once `after` has passed (null: at once), copy `pieces`, cut into tasks of
   // at most kTaskBytes so that every thread takes a share.  Job `j` must be
   // idle (wait(j) returned since its last submit).
@@ -169,6 +171,15 @@ class HostPool {
 
  private:
   static constexpr size_t kTaskBytes = 2u << 20;
+  void stop_all() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();  // the queue is drained first
+    th_.clear();
+  }
   struct Task {
     size_t job;
     hipEvent_t after;
@@ -735,7 +746,13 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
   Inputs in(p, stage && pageable, stage && paged_parity);
   // (the first chunk of a staged call comes in directly, so whole too)
   const bool whole_direct = pageable && !selective;
-  const bool whole_chunks = whole_direct && !stage;
+  // Staged, the pool copies each run into the staging buffer at the slot's
+  // offsets and every run then goes up as its own copy: with large blocks
+  // that saves the lost blocks' PCIe bytes (1/k of a PCIe-bound leg); with
+  // small ones (config 4: k=32+1 x 4 KiB, two runs per stripe) the per-copy
+  // cost would dominate, so below kSelectiveCopyBytes the whole chunk is
+  // staged and goes up as one copy, as unstaged.
+  const bool whole_chunks = whole_direct && (!stage || bs < kSelectiveCopyBytes);
   // D2H of the rebuilt blocks of `chunk` (only those: a survivor's bytes are
   // already in the caller's buffer)
   auto out = [&](size_t chunk, size_t slot) {

@@ -369,32 +369,32 @@ int group_lanes(uint64_t bs, bool head = true) {
 }
 
 template <template <int> class K, typename... A>
-void launch_grouped(int g, uint64_t nblocks, hipStream_t s, A... args) {
+hipError_t launch_grouped(int g, uint64_t nblocks, hipStream_t s, A... args) {
   const uint64_t waves = (nblocks + (64 / g) - 1) / (64 / g);
   const uint32_t grid = grid_for(waves, 0, 64);
   switch (g) {
-    case 1: K<1>::launch(grid, s, args...); break;
-    case 2: K<2>::launch(grid, s, args...); break;
-    case 4: K<4>::launch(grid, s, args...); break;
-    case 8: K<8>::launch(grid, s, args...); break;
-    case 16: K<16>::launch(grid, s, args...); break;
-    case 32: K<32>::launch(grid, s, args...); break;
-    default: K<64>::launch(grid, s, args...); break;
+    case 1: return K<1>::go(grid, s, args...);
+    case 2: return K<2>::go(grid, s, args...);
+    case 4: return K<4>::go(grid, s, args...);
+    case 8: return K<8>::go(grid, s, args...);
+    case 16: return K<16>::go(grid, s, args...);
+    case 32: return K<32>::go(grid, s, args...);
+    default: return K<64>::go(grid, s, args...);
   }
 }
 
 template <int G>
 struct ValidateK {
-  static void launch(uint32_t grid, hipStream_t s, const uint8_t* d, uint64_t n, uint64_t bs,
-                     uint32_t* bad) {
-    wave_validate_kernel<G><<<grid, 64, 0, s>>>(d, n, bs, bad);
+  static hipError_t go(uint32_t grid, hipStream_t s, const uint8_t* d, uint64_t n, uint64_t bs,
+                       uint32_t* bad) {
+    return launch(wave_validate_kernel<G>, grid, 64, 0, s, d, n, bs, bad);
   }
 };
 template <int G>
 struct PatternK {
-  static void launch(uint32_t grid, hipStream_t s, uint8_t* d, uint64_t n, uint64_t bs,
-                     uint64_t seed) {
-    wave_pattern_kernel<G><<<grid, 64, 0, s>>>(d, n, bs, seed);
+  static hipError_t go(uint32_t grid, hipStream_t s, uint8_t* d, uint64_t n, uint64_t bs,
+                       uint64_t seed) {
+    return launch(wave_pattern_kernel<G>, grid, 64, 0, s, d, n, bs, seed);
   }
 };
 
@@ -404,35 +404,29 @@ thread_local int g_validate_mode = 0;  // 0 auto, 1 lane, 2 grouped (xec_set_val
 
 hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t seed,
                           hipStream_t s) {
-  const hipError_t before = hipPeekAtLastError();
   if (nblocks == 0) return hipSuccess;
   uint8_t* d = static_cast<uint8_t*>(d_data);
   const int g = group_lanes(bs);
   // The lane kernel wins once there are lanes enough for every block: its PCG
   // walk needs no jumps (config 4, 2 M blocks: 6.2 vs 14.6 ms, profiles/r02e).
   const bool grouped = g && (g_validate_mode == 2 || (g_validate_mode == 0 && nblocks < kLaneBlocks));
-  if (grouped)
-    launch_grouped<PatternK>(g, nblocks, s, d, nblocks, bs, seed);
-  else
-    serial_pattern_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(d, nblocks, bs, seed);
-  return launch_status(before);
+  if (grouped) return launch_grouped<PatternK>(g, nblocks, s, d, nblocks, bs, seed);
+  return launch(serial_pattern_kernel, (uint32_t)((nblocks + 255) / 256), 256, 0, s, d, nblocks,
+                bs, seed);
 }
 
 hipError_t launch_validate(const void* d_data, uint64_t nblocks, uint64_t bs, uint32_t* d_bad,
                            hipStream_t s) {
-  const hipError_t before = hipPeekAtLastError();
-  if (hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
+  const hipError_t z = hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s);
+  if (z != hipSuccess) return z;
   if (nblocks == 0) return hipSuccess;
   const uint8_t* d = static_cast<const uint8_t*>(d_data);
   const int g = group_lanes(bs, false);
   // Grouped lanes read each segment with 16-B loads a lane walks in order;
   // the lane kernel's strided walk loses even with 2 M blocks (profiles/r02e).
-  if (g && g_validate_mode != 1)
-    launch_grouped<ValidateK>(g, nblocks, s, d, nblocks, bs, d_bad);
-  else
-    serial_validate_kernel<<<(uint32_t)((nblocks + 255) / 256), 256, 0, s>>>(d, nblocks, bs,
-                                                                            d_bad);
-  return launch_status(before);
+  if (g && g_validate_mode != 1) return launch_grouped<ValidateK>(g, nblocks, s, d, nblocks, bs, d_bad);
+  return launch(serial_validate_kernel, (uint32_t)((nblocks + 255) / 256), 256, 0, s, d, nblocks,
+                bs, d_bad);
 }
 
 // Loads this file's code object onto the current device (see xec_kernels.h).

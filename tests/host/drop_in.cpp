@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <new>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -37,13 +38,34 @@
 
 namespace {
 
+// 64-B aligned host memory: the oracle checks XOREC_ALIGNMENT as the
+// reference does (xorec_utils.hpp:61-86)
+template <class T>
+struct Aligned64 {
+  using value_type = T;
+  Aligned64() = default;
+  template <class U>
+  Aligned64(const Aligned64<U>&) {}
+  T* allocate(size_t n) {
+    void* p = std::aligned_alloc(64, (n * sizeof(T) + 63) / 64 * 64);
+    if (p == nullptr) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) { std::free(p); }
+  template <class U>
+  bool operator==(const Aligned64<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const Aligned64<U>&) const { return false; }
+};
+using Bytes = std::vector<uint8_t, Aligned64<uint8_t>>;
+
 template <class P>
 class Probe : public P {
  public:
   using P::P;
   size_t S() const { return this->m_chunks; }
   const uint8_t* bitmap() const { return this->m_block_bitmap.get(); }
-  bool read(std::vector<uint8_t>& d, std::vector<uint8_t>& p) const {
+  bool read(Bytes& d, Bytes& p) const {
     d.assign(this->m_chunks * this->m_chunk_data_size, 0);
     p.assign(this->m_chunks * this->m_chunk_parity_size, 0);
     if constexpr (std::is_same_v<P, XorecBenchmarkHipMulti>) {
@@ -83,7 +105,7 @@ int run(const BenchmarkConfig& c, bool seeded, uint64_t seed, int iterations) {
   }
   AbstractBenchmark& bench = *probe;  // BM_generic sees the interface only
   const size_t S = probe->S();
-  std::vector<uint8_t> d0, p0, d1, p1, d2, p2, want(S * m * bs);
+  Bytes d0, p0, d1, p1, d2, p2, want(S * m * bs);
   for (int it = 1; it <= iterations; ++it) {
     bench.setup();
     if (bench.encode() != 0) return fail("encode() != 0", it);
