@@ -41,6 +41,13 @@ struct Geo {
   // once are read at different offsets -- mixes the address bits of the
   // concurrently read blocks, where `perm` only changed which rows are in flight
   uint64_t rot = 0;
+  // rows grouped: row r starts at (r / sub_rows) * row_stride + (r % sub_rows) *
+  // sub_stride (encode with m > 1: the m classes of a stripe are rows 1 block
+  // apart, stripes k blocks apart); 0 = rows row_stride apart
+  uint64_t sub_rows = 0, sub_stride = 0;
+  // XOR swizzle: row r's chunk c reads column
+  // c ^ ((r * swz) mod tiles_per_row) (tiles_per_row a power of two)
+  uint64_t swz = 0;
 };
 
 __device__ __forceinline__ uint64_t row_of(uint64_t r, const Geo& g) {
@@ -61,8 +68,11 @@ __global__ __launch_bounds__(64) void read_kernel(const uint8_t* __restrict__ ba
   if (t0 >= g.total_tiles) return;
   const uint64_t t = g.reverse ? g.total_tiles - 1 - t0 : t0;
   const uint64_t r = row_of(t / g.tiles_per_row, g);
-  const uint64_t c = (t % g.tiles_per_row + r * g.rot) % g.tiles_per_row;
-  const uint8_t* p = base + r * g.row_stride + (r & 1) * g.alt_offset + c * 1024 + threadIdx.x * 16;
+  uint64_t c = (t % g.tiles_per_row + r * g.rot) % g.tiles_per_row;
+  if (g.swz) c ^= (r * g.swz) & (g.tiles_per_row - 1);
+  const uint64_t row_base = g.sub_rows ? (r / g.sub_rows) * g.row_stride + (r % g.sub_rows) * g.sub_stride
+                                       : r * g.row_stride + (r & 1) * g.alt_offset;
+  const uint8_t* p = base + row_base + c * 1024 + threadIdx.x * 16;
   u32x4 v[NM];
 #pragma unroll
   for (int q = 0; q < NM; ++q) {
@@ -186,6 +196,26 @@ int main(int argc, char** argv) {
                      {8 * MiB, 2 * MiB, 1024, T4, 1, 0, 0, R}});
   // the encode's geometry rotated: must not lose (config 3)
   cases.push_back({"cfg3_16x1MiB_rot64", 16, true, {16 * MiB, MiB, 1024, T16, 1, 0, 0, 64}});
+  // 32+4 x 1 MiB (the reference's (36/32) EC at the north star's shard size,
+  // VERDICT r04 item 4): encode reads 8 members 4 MiB apart per class, the 4
+  // classes of a stripe 1 MiB apart, stripes 32 MiB apart -- the same rows as
+  // the random-loss decode's list tiles (one lost member of each class swapped
+  // for its parity block; 7 of 8 loads keep this geometry)
+  const uint64_t T8e = 4 * GiB / (8 * KiB);
+  cases.push_back({"e32p4_8x4MiB", 8, true, {32 * MiB, 4 * MiB, 1024, T8e, 1, 0, 0, 0, 4, MiB}});
+  cases.push_back({"e32p4_8x4MiB_fwd", 8, true, {32 * MiB, 4 * MiB, 1024, T8e, 0, 0, 0, 0, 4, MiB}});
+  for (uint64_t R : {1ull, 3ull, 64ull, 257ull})
+    cases.push_back({"e32p4_rowrot" + std::to_string(R), 8, true,
+                     {32 * MiB, 4 * MiB, 1024, T8e, 1, 0, 0, R, 4, MiB}});
+  for (uint64_t X : {1ull, 0x9E37ull, 0x2D5ull, 0x155ull})
+    cases.push_back({"e32p4_swz" + std::to_string(X), 8, true,
+                     {32 * MiB, 4 * MiB, 1024, T8e, 1, 0, 0, 0, 4, MiB, X}});
+  // 16+2 x 1 MiB encode for comparison: 8 members 2 MiB apart, 2 classes 1 MiB apart
+  cases.push_back({"e16p2_8x2MiB", 8, true, {16 * MiB, 2 * MiB, 1024, T8e, 1, 0, 0, 0, 2, MiB}});
+  // the same 8 members as one contiguous 8 MiB run per class (no stride)
+  cases.push_back({"e32p4_contig_8x1MiB", 8, true, {8 * MiB, MiB, 1024, T8e, 1, 0}});
+  // cfg3's encode with the swizzle (the 16+1 shape must not lose)
+  cases.push_back({"cfg3_16x1MiB_swz0x9E37", 16, true, {16 * MiB, MiB, 1024, T16, 1, 0, 0, 0, 0, 0, 0x9E37}});
 
   // Every byte a case reads must lie inside the buffers: the last tile's last
   // member ends at (rows-1)*row_stride + tiles_per_row*1 KiB + (nm-1)*member_stride.
@@ -193,8 +223,11 @@ int main(int argc, char** argv) {
   uint64_t need = 0;
   auto end_of = [](const Case& cs) {
     const uint64_t rows = (cs.g.total_tiles + cs.g.tiles_per_row - 1) / cs.g.tiles_per_row;
-    return (rows - 1) * cs.g.row_stride + cs.g.alt_offset + cs.g.tiles_per_row * 1024 +
-           (uint64_t)(cs.nm - 1) * cs.g.member_stride;
+    const uint64_t last_row =
+        cs.g.sub_rows ? ((rows - 1) / cs.g.sub_rows) * cs.g.row_stride +
+                            (cs.g.sub_rows - 1) * cs.g.sub_stride
+                      : (rows - 1) * cs.g.row_stride + cs.g.alt_offset;
+    return last_row + cs.g.tiles_per_row * 1024 + (uint64_t)(cs.nm - 1) * cs.g.member_stride;
   };
   for (const Case& cs : cases) need = std::max(need, end_of(cs));
   need = std::max(need, GiB);  // the write streams cover exactly 1 GiB
