@@ -174,7 +174,16 @@ def rocprof_avg_ns(traffic_src, kernel_base):
     return None
 
 
-def roofline(kernel, b, ms_hip, hbm, traffic_src):
+def build_id_of(info):
+    """The "src:<id>" token of an xec_build_info() string: the hash of the
+    sources the library was built from (erasure-code-benchmark_amd/Makefile)."""
+    for tok in (info or "").split():
+        if tok.startswith("src:"):
+            return tok[4:]
+    return None
+
+
+def roofline(kernel, b, ms_hip, hbm, traffic_src, lib_build_id=None):
     """SURVEY.md §8(d) roofline of one kernel: `achieved` = algorithmic bytes
     per launch / the kernel's rocprofv3 average duration (AverageNs of the
     kernel-stats CSV the traffic file names, so the line's frac is
@@ -198,6 +207,11 @@ def roofline(kernel, b, ms_hip, hbm, traffic_src):
         r["rocprof_over_hip_events_ms"] = round(prof["avg_ns"] * 1e-6 / ms_hip, 4)
     if traffic_src and hbm is not None:
         r["traffic_source"] = traffic_src.get("source")
+    if traffic_src:  # which library the profile measured, and the one this line ran
+        r["profile_build_id"] = traffic_src.get("build_id")
+        r["library_build_id"] = lib_build_id
+        r["profile_is_this_library"] = (lib_build_id is not None and
+                                        traffic_src.get("build_id") == lib_build_id)
     return r
 
 
@@ -1050,8 +1064,9 @@ def run_rank(args):
             traffic_src, traffic, traffic_dec = None, None, None  # profiled at one erasure
         # the dominant kernel is the one the step spends longer in (decode at the
         # BASELINE shapes: in-place writes); both are reported
-        rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic, traffic_src),
-              "decode": roofline(dec_kernel, b_dec, dec_ms, traffic_dec, traffic_src)}
+        lib_id = build_id_of(xec.build_info()) if not args.rehearse_cpu else None
+        rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic, traffic_src, lib_id),
+              "decode": roofline(dec_kernel, b_dec, dec_ms, traffic_dec, traffic_src, lib_id)}
         dominant = ("decode" if rl["decode"]["avg_launch_ms"] >= rl["encode"]["avg_launch_ms"]
                     else "encode")
         cpu = None

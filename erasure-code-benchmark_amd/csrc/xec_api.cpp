@@ -1115,6 +1115,10 @@ const char* xec_status_string(xec_status s) {
   return "Unknown";
 }
 
-const char* xec_build_info(void) { return "xec-hip gfx950 " __DATE__ " " __TIME__; }
+#ifndef XEC_SRC_ID
+#define XEC_SRC_ID "unknown"
+#endif
+// "src:<id>": the hash of the library's sources (erasure-code-benchmark_amd/Makefile)
+const char* xec_build_info(void) { return "xec-hip gfx950 src:" XEC_SRC_ID " " __DATE__ " " __TIME__; }
 
 }  // extern "C"

@@ -14,6 +14,9 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$R"
+# the library this profile measures (its source hash: erasure-code-benchmark_amd/Makefile)
+python3 -c "import sys; sys.path.insert(0, 'erasure-code-benchmark_amd'); import xec; print(xec.build_info())" \
+  > "$OUT/build_info.txt"
 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats -d "$OUT/trace" -o kt --output-format csv \
   -- python3 bench.py --no-cpu-baseline "$@" > "$OUT/bench_trace.log" 2>&1
 for C in FETCH_SIZE WRITE_SIZE; do

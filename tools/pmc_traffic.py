@@ -35,6 +35,21 @@ def short(name: str) -> str:
     return name.split("(")[0].replace("void ", "")
 
 
+def build_id_of(info: str | None) -> str | None:
+    """The "src:<id>" token of an xec_build_info() string (None if absent)."""
+    for tok in (info or "").split():
+        if tok.startswith("src:"):
+            return tok[4:]
+    return None
+
+
+def git_head() -> str | None:
+    import subprocess
+    r = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short=12", "HEAD"],
+                       capture_output=True, text=True)
+    return r.stdout.strip() or None
+
+
 def per_kernel(csv_path: Path) -> dict[str, list[float]]:
     agg: dict[str, list[float]] = {}
     for r in csv.DictReader(open(csv_path)):
@@ -86,7 +101,12 @@ def main():
             "rocprof_calls": int(st["Calls"]) if st else None,
             "achieved_GBps_algorithmic": round(algo[base] / avg_ns, 1) if avg_ns else None,
         }
-    out = {"tag": tag, "workload": workload, "k": k, "m": m, "block_bytes": bs, "stripes": S,
+    info_f = src / "build_info.txt"
+    build_info = info_f.read_text().strip() if info_f.exists() else None
+    build_id = build_id_of(build_info)
+    out = {"tag": tag, "build_info": build_info, "build_id": build_id,
+           "git_head_at_collection": git_head(),
+           "workload": workload, "k": k, "m": m, "block_bytes": bs, "stripes": S,
            "lost_per_stripe": lost,
            "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE halves 16-B streams)",
            "kernels": kernels}
@@ -94,6 +114,9 @@ def main():
     enc = [v for n, v in kernels.items() if n.startswith("xec::encode_kernel")]
     if enc and workload in WORKLOADS:
         traffic = {"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)",
+                   # the library the profile measured (xec_build_info "src:<id>"): bench.py
+                   # reports whether it is the library the line ran
+                   "build_id": build_id,
                    # the same session's kernel trace: bench.py's roofline.achieved /
                    # frac are algorithmic bytes / its AverageNs (bench.rocprof_avg_ns)
                    "timing_source": f"profiles/{tag}_kernel_stats.csv",
