@@ -1,4 +1,4 @@
-# A/B of tools/ab/patches/decode_block_wave.py builds at config 4.
+# A/B of tools/archive/ab/patches/decode_block_wave.py builds at config 4.
 set -e
 out=gpurun_out/${1:-r02av}
 mkdir -p $out

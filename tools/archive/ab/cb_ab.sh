@@ -1,4 +1,4 @@
-# Stores batched over CB chunks per workgroup (tools/ab/patches/chunk_batch.py)
+# Stores batched over CB chunks per workgroup (tools/archive/ab/patches/chunk_batch.py)
 # against the tree, in one process.
 set -e
 out=gpurun_out/${1:-r03o}

@@ -1,8 +1,8 @@
 #!/bin/bash
-# classes-innermost tile order (tools/ab/patches/class_inner.py) against the
+# classes-innermost tile order (tools/archive/ab/patches/class_inner.py) against the
 # product, in one process per shape: encode, single-erasure decode (automatic
 # tiling) and, at every class lost, class-tile decode.
-# Usage (inside gpurun): bash tools/ab/class_inner_ab.sh <out-dir>
+# Usage (inside gpurun): bash tools/archive/ab/class_inner_ab.sh <out-dir>
 set -euo pipefail
 o=${1:?out dir}; mkdir -p "$o"
 for w in 16,2,1048576,256 8,2,1048576,256 16,4,1048576,256 32,4,1048576,256 16,2,4194304,64 \

@@ -1,4 +1,4 @@
-# DIAGNOSTIC run of tools/ab/patches/decode_dst_diag.py builds (see there).
+# DIAGNOSTIC run of tools/archive/ab/patches/decode_dst_diag.py builds (see there).
 set -e
 out=gpurun_out/${1:-r02aq}
 mkdir -p $out

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Residency at finer steps than whole waves per SIMD: times the product
-encode/decode of an XEC_LDS_BYTES-aware build (tools/ab/patches/
+encode/decode of an XEC_LDS_BYTES-aware build (tools/archive/ab/patches/
 lds_env_override.py, built as tools/ab/libxec_ldsenv.so) for several LDS
 reservations per workgroup, interleaved in one process.
 
-    python tools/ab/lds_sweep.py --workload cfg3 --lds 0,20480,16384,13312
+    python tools/archive/ab/lds_sweep.py --workload cfg3 --lds 0,20480,16384,13312
 """
 from __future__ import annotations
 

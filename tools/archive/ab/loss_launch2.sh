@@ -1,4 +1,4 @@
-# Second box for tools/ab/loss_launch.sh's candidates: 2 KiB tiles per wave at
+# Second box for tools/archive/ab/loss_launch.sh's candidates: 2 KiB tiles per wave at
 # 1-2 waves per SIMD against the default, at 8 members per class and m >= 2
 # (and 8+2 for 4 members), blocks 512 KiB - 4 MiB, three loss patterns.
 set -e

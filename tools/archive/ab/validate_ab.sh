@@ -1,4 +1,4 @@
-# Grouped validate kernel at more resident waves (tools/ab/patches/validate_waves.py)
+# Grouped validate kernel at more resident waves (tools/archive/ab/patches/validate_waves.py)
 # against the tree: tools/validate_cost.py per library, alternated twice.
 set -e
 out=gpurun_out/${1:-r03zj}

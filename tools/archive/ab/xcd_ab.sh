@@ -1,4 +1,4 @@
-# A/B of tools/ab/patches/xcd_items.py builds (one item per XCD).
+# A/B of tools/archive/ab/patches/xcd_items.py builds (one item per XCD).
 set -e
 out=gpurun_out/${1:-r02as}
 mkdir -p $out
