@@ -59,6 +59,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--seed", type=int, default=1896)
     ap.add_argument("--rotation", type=int, default=0, help="xec_set_rotation (0 automatic)")
+    ap.add_argument("--occ", default="",
+                    help="comma list of xec_set_occupancy values timed in interleaved rounds "
+                         "(0 automatic, 8 no cap); default: the automatic choice only")
+    ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -97,12 +101,28 @@ def main():
         torch.cuda.synchronize()
         return statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(args.iters))
 
-    # the decode's parity stays as encode left it: re-encode only before the
-    # encode timing, decode timing after (decode never writes parity)
-    te = run(lambda: xec.encode(d, p, S, bs, k, m, s))
-    td = run(lambda: xec.decode(d, p, S, bs, k, m, h, scratch, s))
     b_enc = S * (k + m) * bs
     b_dec = lost_data * (k // m + 1) * bs  # each rebuild reads k/m blocks, writes 1
+    if args.occ:  # residency A/B: every value timed in each round, rounds interleaved
+        occs = [int(x) for x in args.occ.split(",")]
+        te = {o: [] for o in occs}
+        td = {o: [] for o in occs}
+        for _ in range(args.rounds):
+            for o in occs:
+                assert xec.set_occupancy(o) == 0
+                te[o].append(run(lambda: xec.encode(d, p, S, bs, k, m, s)))
+                td[o].append(run(lambda: xec.decode(d, p, S, bs, k, m, h, scratch, s)))
+        assert xec.set_occupancy(0) == 0
+        for o in occs:
+            e, dd = statistics.median(te[o]), statistics.median(td[o])
+            print(json.dumps({"shape": args.shape, "pattern": args.pattern, "occupancy": o,
+                              "encode_ms": round(e, 4), "encode_GBps": round(b_enc / e / 1e6, 1),
+                              "decode_ms": round(dd, 4), "decode_GBps": round(b_dec / dd / 1e6, 1),
+                              "decode_tiling": tiling, "exact": exact}), flush=True)
+        return
+    # the decode's parity stays as encode left it (decode never writes parity)
+    te = run(lambda: xec.encode(d, p, S, bs, k, m, s))
+    td = run(lambda: xec.decode(d, p, S, bs, k, m, h, scratch, s))
     print(json.dumps({"shape": args.shape, "pattern": args.pattern, "rotation": args.rotation,
                       "lost_data_blocks": lost_data, "decode_tiling": tiling, "exact": exact,
                       "encode_ms": round(te, 4), "encode_GBps": round(b_enc / te / 1e6, 1),
