@@ -57,3 +57,38 @@ def test_frac_falls_back_to_hip_events_without_a_profile():
     src = json.loads((ROOT / "profiles" / "traffic_cfg3.json").read_text())
     r = bench.roofline("xec::decode_class_kernel", 8_000_000_000, 1.0, None, src)
     assert r["timing_source"].startswith("HIP events")
+
+
+def _source_id():
+    """erasure-code-benchmark_amd/Makefile's XEC_SRC_ID: sha256 of the library's
+    sources (sorted csrc/*.hip, *.cpp, *.h), include/xec.h and the Makefile."""
+    import hashlib
+    pkg = ROOT / "erasure-code-benchmark_amd"
+    files = sorted(str(p.relative_to(pkg)) for pat in ("*.hip", "*.cpp", "*.h")
+                   for p in (pkg / "csrc").glob(pat))
+    h = hashlib.sha256()
+    for f in files + [str(ROOT / "include" / "xec.h"), "Makefile"]:
+        h.update((pkg / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def test_library_build_id_is_its_sources():
+    """xec_build_info()'s "src:<id>" is the hash of the sources in the tree, so
+    the id names what the library was built from (no stale .so)."""
+    import xec
+    assert bench.build_id_of(xec.build_info()) == _source_id()
+
+
+@pytest.mark.parametrize("workload", sorted(bench.WORKLOADS))
+def test_profile_is_the_shipped_library(workload):
+    """the profile behind the line's frac recorded the
+    build id of the library that ships; bench.py reports the comparison."""
+    import xec
+    lib = bench.build_id_of(xec.build_info())
+    _, src = bench.load_traffic(workload)
+    assert lib and src.get("build_id") == lib, (src.get("build_id"), lib)
+    pmc = json.loads((ROOT / src["source"].split(" ")[0]).read_text())
+    assert pmc["build_id"] == lib
+    assert (ROOT / src["timing_source"]).exists()
+    r = bench.roofline("xec::encode_kernel", 1, 1.0, None, src, lib)
+    assert r["profile_is_this_library"] is True and r["profile_build_id"] == lib
