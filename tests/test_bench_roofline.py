@@ -40,7 +40,8 @@ def test_frac_recomputes_from_cited_profile(workload):
                          (dec_base, b_dec, src["decode_hbm_bytes_per_launch"])):
         r = bench.roofline(base, b, 1.0, hbm, src)
         avg_ns = float(_row(src["timing_source"], base)["AverageNs"])
-        assert round(b / avg_ns / 8000.0, 3) == round(r["frac"], 3)
+        # r["frac"] = round(achieved to 0.1 GB/s) / peak, to 4 places
+        assert abs(b / avg_ns / 8000.0 - r["frac"]) < 1e-4
         assert r["avg_launch_ms"] == round(avg_ns * 1e-6, 4)
         assert src["timing_source"] in r["timing_source"]
         # the HIP-event figure of this (made-up) run is kept beside it

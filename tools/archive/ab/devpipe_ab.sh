@@ -12,7 +12,7 @@ SH=16,1,1048576,2048:32,1,4096,65536:16,8,65536,16384:16,2,1048576,256
 for pat in $pats; do
   for lib in $libs; do
     if [ $lib = tree ]; then unset XEC_LIB; else export XEC_LIB=$PWD/tools/ab/libxec_$lib.so; fi
-    timeout -k 10 400 python -u tools/tiling_ab.py --device --shapes $SH --lost 1 --pattern $pat \
+    timeout -k 10 400 python -u tools/archive/tiling_ab.py --device --shapes $SH --lost 1 --pattern $pat \
       --variants dev,devlist --rounds 5 --iters 8 --out $out/devpipe_${lib}_${pat}.json \
       > $out/devpipe_${lib}_${pat}.log 2>&1
     python3 -c "

@@ -14,7 +14,7 @@ def main():
     out = ["# Published GPU rows of the reference: results/raw/final_results.csv, every",
            "# \"XOR-EC (GPU Computation)\" row (kenji-k6/erasure-code-benchmark, Tesla V100,",
            "# 500 iterations after 100 warm-up), with their file line numbers. Data only;",
-           "# regenerate with tools/extract_reference_rows.py.",
+           "# regenerate with tools/archive/extract_reference_rows.py.",
            "line," + lines[0]]
     out += [f"{i},{ln}" for i, ln in enumerate(lines[1:], start=2)
             if ln.startswith('"XOR-EC (GPU Computation)"')]

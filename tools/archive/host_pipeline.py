@@ -8,7 +8,7 @@ The batch starts and ends in pinned host memory.  Measured:
 Rates are in the reference's convention (data bytes / s, GB = 1e9), the
 natural unit for a path whose bytes cross PCIe once.
 
-    python tools/host_pipeline.py [--workload cfg3|k,m,bs,S] [--lost N] [--reps 3] [--out f.json]
+    python tools/archive/host_pipeline.py [--workload cfg3|k,m,bs,S] [--lost N] [--reps 3] [--out f.json]
 """
 from __future__ import annotations
 
@@ -19,7 +19,7 @@ import sys
 import time
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 sys.path.insert(0, str(ROOT))
 

@@ -6,7 +6,7 @@ under --marker-trace the range must appear, under --selected-regions only the
 import sys
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[2]
+ROOT = Path(__file__).resolve().parents[3]
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 
 import torch  # noqa: E402

@@ -11,7 +11,7 @@ reference-shaped plugin path.
 3. the decode kernel alone (HIP events around xec_decode launched back to back
    on one stream, so each call's scan overlaps the previous kernel).
 
-    python tools/scan_cost.py [--workload cfg4] [--out f.json]
+    python tools/archive/scan_cost.py [--workload cfg4] [--out f.json]
 """
 from __future__ import annotations
 
@@ -25,7 +25,7 @@ import sys
 import time
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 

@@ -3,7 +3,7 @@
 # library: timed-launch kernel stats + PMC traffic (tools/gpu_profile.sh) of
 # the given shapes; tools/pmc_traffic.py turns gpurun_out/prof_<tag>/ into
 # profiles/.  Shapes are "workload:lost" (bench.py workload name or k,m,bs,S).
-# Usage (inside gpurun): bash tools/shape_table.sh <round-tag> <shape>...
+# Usage (inside gpurun): bash tools/archive/shape_table.sh <round-tag> <shape>...
 set -euo pipefail
 R=${1:?round tag}; shift
 for spec in "$@"; do

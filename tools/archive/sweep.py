@@ -6,7 +6,7 @@ Also times two known-good HBM references on the same device and buffers size:
 torch's device-to-device copy (copy_) and a torch.bitwise_xor of two tensors,
 so kernel fractions can be read against what this box actually sustains.
 
-    python tools/sweep.py [--workload cfg3] [--rounds 5] [--iters 10]
+    python tools/archive/sweep.py [--workload cfg3] [--rounds 5] [--iters 10]
 """
 from __future__ import annotations
 
@@ -17,7 +17,7 @@ import statistics
 import sys
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 sys.path.insert(0, str(ROOT))
 

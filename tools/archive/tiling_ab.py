@@ -16,7 +16,7 @@ fraction --fraction of the stripes, spread evenly over the batch (stripe c
 keeps its losses when frac(c * 0.618...) < f): the sweep that prices the
 work-list threshold (xec_api.cpp kListStripesNum / kListStripesDen).
 
-    python tools/tiling_ab.py [--shapes 16,2,1048576,256:16,8,65536,16384]
+    python tools/archive/tiling_ab.py [--shapes 16,2,1048576,256:16,8,65536,16384]
                               [--pattern uniform|sparse|skew] [--out f.json]
 """
 from __future__ import annotations
@@ -27,7 +27,7 @@ import statistics
 import sys
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 

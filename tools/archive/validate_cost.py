@@ -10,7 +10,7 @@ Validation must read every data byte once (S*k*bs), so its floor is the HBM
 read time of the data -- about the encode's own time, which reads the same
 bytes and writes 1/k more.
 
-    python tools/validate_cost.py [--workload cfg3] [--iters 10] [--out f.json]
+    python tools/archive/validate_cost.py [--workload cfg3] [--iters 10] [--out f.json]
 """
 from __future__ import annotations
 
@@ -20,7 +20,7 @@ import statistics
 import sys
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 
