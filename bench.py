@@ -452,9 +452,11 @@ def cpu_baseline(workload, k, m, bs, S_gpu, budget_s, numa_node=None,
     out["nproc"] = nproc
     out["omp_num_threads"] = omp
     out["cgroup_cpu_quota"] = quota
-    out["spread_note"] = ("min / max: the spread within this run; between boxes the same "
-                          "binding measured 266-382 GB/s at cfg3 in round 4 (which NUMA node "
-                          "holds the GPU, and the shared host's other load; DESIGN.md §4)")
+    out["spread_note"] = ("min / max: the spread within this run; value is the fastest of the "
+                          "placements timed here (placements); between boxes the GPU-node "
+                          "binding measured 266-382 GB/s at cfg3 in round 4 and the placements "
+                          "of one box 302-517 in round 5 (which NUMA node holds the GPU, and "
+                          "the shared host's other load; DESIGN.md §4)")
     out["binding"] = {"OMP_PROC_BIND": "close", "OMP_PLACES": places, "cpus": cpus,
                       "gpu_numa_node": numa_node,
                       "note": "one thread per physical core of the GPU's NUMA node, spread "

@@ -32,6 +32,9 @@ from bench import HOST_CHUNK_STRIPES, HOST_STREAMS, erasure_pattern  # noqa: E40
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stripes", type=int, default=64)
+    ap.add_argument("--shape", default="16,1,1048576",
+                    help="k,m,bs (default config 3's; config 4: 32,1,4096 with --stripes 8192 "
+                         "--chunk 1024)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=HOST_CHUNK_STRIPES)
     ap.add_argument("--streams", type=int, default=HOST_STREAMS)
@@ -54,7 +57,8 @@ def main():
 
     torch.cuda.set_device(0)
     assert xec.init(0) == 0
-    k, m, bs, S = 16, 1, 1 << 20, args.stripes
+    k, m, bs = (int(x) for x in args.shape.split(","))
+    S = args.stripes
     nbytes = S * k * bs
     s = torch.cuda.current_stream()
     d_d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -64,7 +68,8 @@ def main():
     ref_d, ref_p = d_d.cpu(), d_p.cpu()
     bm = erasure_pattern(np, S, k, m)
     h_bm = torch.from_numpy(bm.reshape(-1)).pin_memory()
-    out = {"shape": f"k={k}+{m}, 1 MiB x {S} stripes ({nbytes >> 20} MiB data)",
+    out = {"shape": f"k={k}+{m}, {bs >> 10} KiB x {S} stripes ({nbytes >> 20} MiB data)",
+           "library": xec.build_info(),
            "pipeline": f"{args.chunk}-stripe chunks x {args.streams} streams"}
 
     def best(fn, before=None):
