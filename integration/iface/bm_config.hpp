@@ -1,17 +1,15 @@
-// bm_config.hpp -- this repository's restatement of the reference's
-// src/benchmark/bm_config.hpp:1-57: the per-run BenchmarkConfig every plugin
-// constructor takes, the KiB / MiB literal macros and the sweep vectors
-// (defined in bm_config.cpp, as the reference's src/benchmark/bm_config.cpp:3-23).
-//
-// The reference pulls ConsoleReporter and benchmark::State in through Google
-// Benchmark (console_reporter.hpp); the config only names them as incomplete
-// types, so they are declared here and nothing else of Google Benchmark is
-// needed.
+// bm_config.hpp -- this repository's restatement of the reference's per-run
+// configuration header (src/benchmark/bm_config.hpp:1-57), for builds where the
+// reference is not mounted.  What a plugin sees of it:
+//   * BenchmarkConfig -- the fields of bm_config.hpp:25-43, same names, types,
+//     order and defaults (plugin constructors take one);
+//   * the KiB / MiB literal suffix macros, ECTuple = (total blocks, data
+//     blocks), MESSAGE_SIZE and the sweep vectors (defined in bm_config.cpp);
+//   * BenchmarkFunction, whose benchmark::State parameter (Google Benchmark)
+//     and the ConsoleReporter pointer are only named, never used: both are
+//     declared as incomplete types here.
 #ifndef BM_CONFIG_HPP
 #define BM_CONFIG_HPP
-
-#define KiB *1024
-#define MiB *1024*1024
 
 #include <cstddef>
 #include <cstdint>
@@ -20,32 +18,32 @@
 
 #include "xorec_utils.hpp"
 
+#define KiB *1024
+#define MiB *1024*1024
+
+class ConsoleReporter;
 namespace benchmark {
 class State;
 }
-class ConsoleReporter;
 
-// (total blocks, data blocks) of one stripe, bm_config.hpp:18
 using ECTuple = std::tuple<size_t, size_t>;
 
-// bm_config.hpp:25-43, field for field
 struct BenchmarkConfig {
-  size_t message_size;     // bytes of data per batch (all stripes)
-  size_t block_size;       // bytes per block
-  ECTuple ec_params;       // (k + m, k)
-  size_t num_lost_blocks;  // blocks lost per stripe (data or parity)
-
+  // the batch: message bytes, block bytes, (k + m, k), losses per stripe
+  size_t message_size;
+  size_t block_size;
+  ECTuple ec_params;
+  size_t num_lost_blocks;
+  // host threads of the CPU codecs
   size_t num_cpu_threads;
-
+  // timed and untimed iterations of BM_generic
   int num_iterations;
   int num_warmup_iterations;
-
   XorecVersion xorec_version = XorecVersion::Scalar;
-
+  // GPU codecs; the grid of the reference's CUDA kernels
   bool gpu_computation;
   size_t num_gpu_blocks = 0;
   size_t threads_per_gpu_block = 0;
-
   ConsoleReporter* reporter = nullptr;
 };
 
