@@ -109,8 +109,14 @@ def lib() -> ctypes.CDLL:
         "xec_set_tuning": ([ctypes.POINTER(Tuning)], st),
         "xec_select_lost_blocks": ([sz, sz, sz, vp, ctypes.c_uint64], st),
     }
+    default = "XEC_LIB" not in os.environ
     for name, (args, res) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if default:
+                raise XecLibraryError(f"{LIB_PATH} lacks {name}: rebuild it") from None
+            continue  # an older build under XEC_LIB (in-process A/B, tools/ab): bind what it has
         fn.argtypes = args
         fn.restype = res
     _lib = L
