@@ -32,3 +32,20 @@ def test_plugin_defaults(tmp_path, sanitize):
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "plugin_defaults ok" in p.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_restated_interface_utilities_match_the_oracle(tmp_path):
+    """integration/iface/utils.cpp (the utilities the plugins' one-argument
+    constructor uses) against the oracle: PCG32, the validation payload and
+    checksum, the erasure draw (tests/host/iface_utils.cpp)."""
+    obj = tmp_path / "oracle.o"
+    subprocess.run(["gcc", "-std=c11", "-O1", "-fopenmp", "-c", str(ROOT / "oracle" / "xorec_oracle.c"),
+                    "-o", str(obj)], check=True)
+    exe = tmp_path / "iface_utils"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fopenmp", "-Wall", "-Wextra", "-Werror",
+                    f"-I{IFACE}", f"-I{ROOT / 'oracle'}",
+                    str(ROOT / "tests" / "host" / "iface_utils.cpp"), str(IFACE / "utils.cpp"),
+                    str(obj), "-o", str(exe)], check=True)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "iface_utils ok" in p.stdout, p.stdout[-3000:] + p.stderr[-3000:]
