@@ -119,6 +119,12 @@ hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, c
                         hipStream_t s);
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,
                        hipStream_t s);
+// Gather (xec_pipeline's small-block decode): block i of stripe c of a chunk
+// (item c << 8 | i, at most kArgItems items, k <= 256) is copied from
+// d_data + (c*k + i)*bs to d_out + g*bs for the g-th item, so the chunk's
+// rebuilt blocks leave in one D2H copy.  bs % 16 == 0.
+hipError_t launch_gather(const void* d_data, void* d_out, uint64_t k, uint64_t bs,
+                         const uint32_t* h_items, uint64_t n, hipStream_t s);
 // xec_set_validate_kernel: 0 auto, 1 lane per block, 2 wave per block.
 extern thread_local int g_validate_mode;
 hipError_t launch_pattern(void* d_data, uint64_t nblocks, uint64_t bs, uint64_t seed,

@@ -444,6 +444,21 @@ __global__ __launch_bounds__(256) void erase_kernel(uint8_t* data, uint8_t* pari
 }
 
 // ---------------------------------------------------------------------------
+// gather: the host pipeline's rebuilt small blocks into one contiguous run
+// (csrc/xec_pipeline.cpp: one D2H copy instead of one per block)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gather_kernel(const uint8_t* __restrict__ data,
+                                                     uint8_t* __restrict__ out, uint64_t k,
+                                                     uint64_t bs, uint32_t n, ArgItems items) {
+  for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
+    const uint32_t item = items.v[g];
+    const uint8_t* src = data + ((uint64_t)(item >> 8) * k + (item & 0xFFu)) * bs;
+    uint8_t* dst = out + (uint64_t)g * bs;
+    for (uint64_t x = threadIdx.x * 16ull; x < bs; x += 256 * 16) st16<false>(dst + x, ld16<true>(src + x));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // fill: splitmix64 stream per stripe, state seed_base + c
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t n) {
@@ -603,6 +618,17 @@ hipError_t launch_erase(void* d_data, void* d_parity, const uint8_t* d_bitmap, c
   const uint32_t grid = grid_for(nblocks, 65536, 256);
   return launch(erase_kernel, grid, 256, 0, s, static_cast<uint8_t*>(d_data),
                 static_cast<uint8_t*>(d_parity), d_bitmap, g);
+}
+
+hipError_t launch_gather(const void* d_data, void* d_out, uint64_t k, uint64_t bs,
+                         const uint32_t* h_items, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n > kArgItems || k == 0 || k > 256 || bs % 16 != 0 || h_items == nullptr)
+    return hipErrorInvalidValue;
+  ArgItems a;
+  std::memcpy(a.v, h_items, n * sizeof(uint32_t));
+  return launch(gather_kernel, grid_for(n, 0, 256), 256, 0, s, static_cast<const uint8_t*>(d_data),
+                static_cast<uint8_t*>(d_out), k, bs, (uint32_t)n, a);
 }
 
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,

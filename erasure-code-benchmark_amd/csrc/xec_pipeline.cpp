@@ -472,6 +472,16 @@ bool for_runs(size_t n, W&& want, F&& copy) {
 // in per-copy overhead than the bytes it saves.  With m = 1 both are the same.
 constexpr size_t kSelectiveCopyBytes = 64u << 10;
 
+// Below this block size a decode's copies are counted, not its bytes: every
+// H2D / D2H command costs ~10 us of SDMA start-up, while the
+// bytes a per-run copy would save -- the lost blocks' -- move in 1/k of a
+// chunk's time.  So a chunk's (non-selective) inputs go up whole and its
+// rebuilt blocks are gathered on the device and come back as one copy
+// (profiles/r05j, r05k: config 4's shape 12.8 -> 52.1 GB/s pinned, 15.5 ->
+// 53.4 pageable).  At 1 MiB blocks per-run copies tie whole ones and save the
+// lost blocks' PCIe bytes, so they stay (config 3: 55 GB/s, the PCIe bound).
+constexpr size_t kWholeCopyBelowBytes = 1u << 20;
+
 // A chunk's outputs (parity, or rebuilt blocks) are queued after the next
 // chunk's inputs rather than right behind its own kernel, so the copy engine
 // has the next chunk's input queued before the host waits on anything.
@@ -740,22 +750,57 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
   // -- ~20 us of host time per call, against the 1/k more bytes (profiles/r03v).
   const bool pageable = !host_pinned(h_data);
   const bool paged_parity = !host_pinned(h_parity);
-  if (pageable && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
+  // Below kWholeCopyBelowBytes one copy per run of survivors in and one per
+  // rebuilt block out cost more than the bytes (config 4's shape: pinned
+  // decode 12.8 GB/s, config 2's 30; tools/pageable_probe.py, profiles/r05j,
+  // r05k).  So there a chunk's non-selective inputs go up whole (pinned or
+  // staged), and its rebuilt blocks are gathered on the device into the
+  // slot's parity region -- free once the decode kernel has read it -- and
+  // leave as ONE D2H copy into the slot's bounce buffer, which the helper
+  // thread scatters (items c << 8 | i: k <= 256).
+  const bool gather = bs < kWholeCopyBelowBytes && k <= 256;
+  if ((pageable || gather) && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
   const bool stage = (pageable || paged_parity) && ensure_stage(p);
   if (!stage && p->opt_pinned_aux) (void)ensure_aux(p);  // without: one stream, as before
   Inputs in(p, stage && pageable, stage && paged_parity);
   // (the first chunk of a staged call comes in directly, so whole too)
-  const bool whole_direct = pageable && !selective;
+  const bool whole_direct = (pageable || bs < kWholeCopyBelowBytes) && !selective;
   // Staged, the pool copies each run into the staging buffer at the slot's
   // offsets and every run then goes up as its own copy: with large blocks
   // that saves the lost blocks' PCIe bytes (1/k of a PCIe-bound leg); with
-  // small ones (config 4: k=32+1 x 4 KiB, two runs per stripe) the per-copy
-  // cost would dominate, so below kSelectiveCopyBytes the whole chunk is
-  // staged and goes up as one copy, as unstaged.
-  const bool whole_chunks = whole_direct && (!stage || bs < kSelectiveCopyBytes);
+  // smaller ones (config 4: k=32+1 x 4 KiB, two runs per stripe) the
+  // per-copy cost would dominate, so below kWholeCopyBelowBytes the whole
+  // chunk is staged and goes up as one copy, as unstaged.
+  const bool whole_chunks = whole_direct && (!stage || bs < kWholeCopyBelowBytes);
   // D2H of the rebuilt blocks of `chunk` (only those: a survivor's bytes are
   // already in the caller's buffer)
+  auto gather_out = [&](size_t chunk, size_t slot) {
+    const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
+    auto& s = p->slots[slot];
+    p->copier->wait_slot(slot);
+    std::vector<uint32_t> items;
+    std::vector<HostCopier::Piece> owed;
+    for (size_t c = c0; c < c0 + n; ++c)
+      for (size_t i = 0; i < k; ++i)
+        if (h_bitmap[c * row + i] == 0) {
+          owed.push_back({data + (c * k + i) * bs, s.bounce + items.size() * bs, bs});
+          items.push_back(static_cast<uint32_t>(((c - c0) << 8) | i));
+        }
+    for (size_t g0 = 0; g0 < items.size(); g0 += xec::kArgItems) {
+      const size_t g = items.size() - g0 < xec::kArgItems ? items.size() - g0 : xec::kArgItems;
+      if (xec::launch_gather(s.data, s.parity + g0 * bs, k, bs, items.data() + g0, g, s.stream) !=
+          hipSuccess)
+        return false;
+    }
+    if (hipMemcpyAsync(s.bounce, s.parity, items.size() * bs, hipMemcpyDeviceToHost, s.stream) !=
+            hipSuccess ||
+        hipEventRecord(s.out_done, s.stream) != hipSuccess)
+      return false;
+    p->copier->push(slot, s.out_done, std::move(owed));
+    return true;
+  };
   auto out = [&](size_t chunk, size_t slot) {
+    if (gather) return gather_out(chunk, slot);
     const size_t c0 = chunk * cs, n = (S - c0) < cs ? (S - c0) : cs;
     auto& s = p->slots[slot];
     std::vector<HostCopier::Piece> owed;

@@ -20,6 +20,11 @@ def _pinned(nbytes):
     # m > 1 at >= 64 KiB blocks: only the classes that lost a data block travel
     (40, 16, 4, 65536, 8, 3, 1), (24, 16, 4, 65536, 5, 2, 2), (12, 8, 2, 1 << 20, 4, 2, 2),
     (9, 24, 8, 65536, 4, 3, 3),
+    # small blocks gather the rebuilt blocks on the device: more than one gather
+    # launch per chunk (> 1,024 rebuilt blocks), and k > 256 (per-block copies)
+    (3001, 4, 4, 256, 1500, 2, 4), (20, 300, 3, 256, 8, 2, 3),
+    # below 1 MiB blocks: selective inputs with gathered outputs, and whole inputs
+    (20, 16, 2, 262144, 4, 2, 2), (33, 8, 1, 524288, 4, 3, 1),
 ])
 def test_pipeline_encode_decode(gpu, oracle, S, k, m, bs, chunk, ns, lost):
     ref_d, ref_p = oracle.batch(S, k, m, bs)

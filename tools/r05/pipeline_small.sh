@@ -10,12 +10,16 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_gpu_pipeline.py tests/test_gpu_error_state.py tests/test_gpu_stream_lifetime.py > $O/pytest.log 2>&1
 tail -1 $O/pytest.log
 for R in 1 2; do
-  for L in tools/ab/libxec_r4final.so erasure-code-benchmark_amd/xec/libxec_hip.so; do
+  for L in ${LIBS:-tools/ab/libxec_r4final.so erasure-code-benchmark_amd/xec/libxec_hip.so}; do
     XEC_LIB=$L timeout -k 10 200 python3 tools/pageable_probe.py --shape 32,1,4096 --stripes 8192 \
       --chunk 1024 --kinds pinned,pageable >> $O/cfg4.log 2>&1
     XEC_LIB=$L timeout -k 10 200 python3 tools/pageable_probe.py --shape 8,1,65536 --stripes 1024 \
       --chunk 128 --kinds pinned,pageable >> $O/cfg2.log 2>&1
     XEC_LIB=$L timeout -k 10 200 python3 tools/pageable_probe.py --kinds pinned,pageable >> $O/cfg3.log 2>&1
+    XEC_LIB=$L timeout -k 10 200 python3 tools/pageable_probe.py --shape 16,4,65536 --stripes 1024 \
+      --chunk 64 --kinds pinned,pageable >> $O/s16p4_64k.log 2>&1
+    XEC_LIB=$L timeout -k 10 200 python3 tools/pageable_probe.py --shape 16,2,262144 --stripes 256 \
+      --chunk 32 --kinds pinned,pageable >> $O/s16p2_256k.log 2>&1
   done
 done
 echo "pipeline_small done"
