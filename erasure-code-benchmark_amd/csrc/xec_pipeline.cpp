@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -625,6 +626,11 @@ static xec_status create_impl(xec_pipeline** out, size_t chunk_stripes, size_t b
   xec_status st = xec_check_args(reinterpret_cast<void*>(64), reinterpret_cast<void*>(64), bs, k, m);
   if (st != XEC_SUCCESS) return st;
   if (chunk_stripes == 0 || nstreams < 1 || nstreams > 16) return XEC_INVALID_SIZE;
+  // a slot's chunk_stripes*(k+m)*bs bytes must be representable (k, m and bs
+  // are bounded by the checks above only from below)
+  const size_t row_bytes = (k + m) * bs;
+  if (k + m < k || row_bytes / bs != k + m || chunk_stripes > SIZE_MAX / row_bytes)
+    return XEC_INVALID_SIZE;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return XEC_DEVICE_ERROR;
   auto* p = new (std::nothrow) xec_pipeline;
@@ -757,8 +763,9 @@ static xec_status decode_impl(xec_pipeline* p, void* h_data, const void* h_parit
   // staged), and its rebuilt blocks are gathered on the device into the
   // slot's parity region -- free once the decode kernel has read it -- and
   // leave as ONE D2H copy into the slot's bounce buffer, which the helper
-  // thread scatters (items c << 8 | i: k <= 256).
-  const bool gather = bs < kWholeCopyBelowBytes && k <= 256;
+  // thread scatters (u32 items c << 8 | i: k <= 256, fewer than 2^24 stripes
+  // per chunk).
+  const bool gather = bs < kWholeCopyBelowBytes && k <= 256 && cs <= (size_t{1} << 24);
   if ((pageable || gather) && !ensure_bounce(p)) return XEC_DEVICE_ERROR;
   const bool stage = (pageable || paged_parity) && ensure_stage(p);
   if (!stage && p->opt_pinned_aux) (void)ensure_aux(p);  // without: one stream, as before

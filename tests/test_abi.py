@@ -269,3 +269,25 @@ def test_select_lost_blocks_matches_oracle(oracle):
     bm = np.ones(5, np.uint8)
     assert xec.select_lost_blocks(4, 1, 2, bm, 0) == xec.Status.INVALID_COUNTS
     assert (bm == 1).all()
+
+
+def test_pipeline_create_rejects_bad_sizes_before_the_device():
+    # argument checks (xorec_utils.hpp:61-86 on bs, k, m) and a slot size
+    # chunk_stripes*(k+m)*bs that must fit a size_t come before any HIP call,
+    # so they answer without a GPU and leave nothing allocated
+    import ctypes
+    L = xec.lib()
+    h = ctypes.c_void_p(123)
+    cases = [
+        ((4, 100, 4, 1, 2), xec.Status.INVALID_SIZE),     # bs not a multiple of 256
+        ((4, 4096, 6, 4, 2), xec.Status.INVALID_COUNTS),  # k % m != 0
+        ((0, 4096, 4, 1, 2), xec.Status.INVALID_SIZE),    # no stripes per chunk
+        ((4, 4096, 4, 1, 0), xec.Status.INVALID_SIZE),    # no streams
+        ((4, 4096, 4, 1, 17), xec.Status.INVALID_SIZE),   # more than 16 streams
+        ((2**62, 4096, 16, 1, 2), xec.Status.INVALID_SIZE),  # slot bytes overflow
+        ((1, 2**60, 32, 32, 2), xec.Status.INVALID_SIZE),    # row bytes overflow
+    ]
+    for args, want in cases:
+        h.value = 123
+        assert xec.Status(L.xec_pipeline_create(ctypes.byref(h), *args)) == want, args
+        assert h.value is None, args  # *out cleared on every failure
