@@ -3,6 +3,9 @@
 # run of survivors; round 5 stages such chunks whole.  Config 4's shape and
 # config 3's, round-4 final library (tools/ab/libxec_r4final.so) against the
 # working tree's, alternating processes, 2 rounds.  Output: gpurun_out/r05j/.
+# tools/ab/libxec_r4final.so (git-ignored) is rebuilt from commit 02ed769:
+#   git worktree add /tmp/r4 02ed769 && make -C /tmp/r4/erasure-code-benchmark_amd \
+#     && cp /tmp/r4/erasure-code-benchmark_amd/xec/libxec_hip.so tools/ab/libxec_r4final.so
 set -euo pipefail
 O=gpurun_out/r05j
 mkdir -p $O

@@ -3,6 +3,9 @@
 # outputs.  Pipeline + error-state GPU tests, then config 4's and config 3's
 # shapes through tools/pageable_probe.py, round-4 final library against the
 # working tree's, alternating processes.  Output: gpurun_out/$1/.
+# tools/ab/libxec_r4final.so (git-ignored) is rebuilt from commit 02ed769:
+#   git worktree add /tmp/r4 02ed769 && make -C /tmp/r4/erasure-code-benchmark_amd \
+#     && cp /tmp/r4/erasure-code-benchmark_amd/xec/libxec_hip.so tools/ab/libxec_r4final.so
 set -euo pipefail
 O=gpurun_out/${1:?tag}
 mkdir -p $O
