@@ -597,7 +597,22 @@ def measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms, reps=
                 S_total * k * bs / (t_sc + enc_ms * 1e-3 + t_ga) / 1e9, 1),
             "gathered_parity_bit_exact_vs_root_encode": ok_ga,
             "note": f"batch starts on rank 0; {dist.get_backend()} send/recv of stripe ranges "
-                    "(RCCL over xGMI with nccl); link-bound"}
+                    "(RCCL with nccl); link-bound; path = how rank 0's GPU reaches the "
+                    "others (topology: xgmi-p2p = peer access over xGMI, staged = none)"}
+
+
+def scatter_topology(devices, rehearse=False):
+    """Config 5's root -> peer pairs as the runtime reports them (xec/topology.py;
+    VERDICT r05 item 2): rank 0's device is the root, `devices` the ranks'
+    devices.  A CPU rehearsal has no runtime to ask: it records the
+    XEC_TOPOLOGY_STUB topology, or says it has none."""
+    from xec import topology
+    if rehearse and not os.environ.get("XEC_TOPOLOGY_STUB"):
+        return {"skipped": "CPU rehearsal: no runtime to ask (set XEC_TOPOLOGY_STUB)"}
+    try:
+        return topology.record(int(devices[0]), [int(d) for d in devices])
+    except Exception as e:  # noqa: BLE001 - a diagnostic field, never the line
+        return {"error": repr(e)[:200]}
 
 
 HOST_CHUNK_STRIPES, HOST_STREAMS = 8, 3  # best measured pipeline shape (DESIGN.md §7)
@@ -1149,6 +1164,12 @@ def run_rank(args):
                     if args.steps >= NSETS else None for q in range(NSETS)]
                 for n, v, shift in (("encode", enc_list, 0), ("decode", dec_list, NSETS - 1))},
         }
+        if world > 1:
+            # how the scatter leg's bytes travel from rank 0's GPU to each rank's
+            # (a CPU rehearsal stands for an N-GPU node: rank r on device r)
+            out["topology"] = scatter_topology(
+                list(range(world)) if args.rehearse_cpu else [int(r[5]) for r in rows],
+                args.rehearse_cpu)
     else:
         out = None
 
@@ -1253,6 +1274,8 @@ def run_rank(args):
                     sc = measure_scatter(torch, dist, ops, S_total, S, start, k, m, bs, enc_ms)
             except Exception as e:  # noqa: BLE001 - report, keep the headline line
                 sc = {"error": repr(e)[:200]}
+            if out is not None:  # rank 0: xgmi-p2p, staged, ... from the topology record
+                sc["path"] = out.get("topology", {}).get("path", "unknown")
             merge("scatter", sc)
         with lock:
             printed.append(True)  # a watchdog firing from here on finds the legs done

@@ -35,6 +35,7 @@ thread_local int g_nt = 0;
 thread_local int g_threads = 0;
 thread_local int g_occupancy = 0;      // waves per SIMD, 0 = automatic
 thread_local int g_decode_tiling = 0;  // 0 auto, 1 stripe, 2 class, 3 list
+thread_local int g_arg_cap_used = 0;   // xec_decode_arg_capacity_used
 thread_local int g_tiling_used = 0;    // xec_decode_tiling_used: this thread's last xec_decode
 thread_local int g_rotation = 0;       // xec_set_rotation: 0 automatic, -1 none, > 0 tiles
 
@@ -659,6 +660,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
                               size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
                               hipStream_t stream) {
   g_tiling_used = 0;
+  g_arg_cap_used = 0;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
@@ -738,6 +740,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
       st = xec_scan_bitmap(h_bitmap, S, k, m, &scan, items, xec::kArgItems);
       if (st != XEC_SUCCESS) return st;
       g_tiling_used = XEC_TILING_ARG_LIST;
+      g_arg_cap_used = (int)xec::arg_items_capacity(scan.lost_data);
       const hipError_t le = xec::launch_decode(d_data, d_parity, nullptr, g, ls,
                                                xec::kDecodeArgListTiles, stream, scan.lost_data,
                                                items);
@@ -828,11 +831,13 @@ xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, s
 }
 
 int xec_decode_tiling_used(void) { return g_tiling_used; }
+int xec_decode_arg_capacity_used(void) { return g_arg_cap_used; }
 
 static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, size_t S, size_t bs,
                                          size_t k, size_t m, const uint8_t* h_bitmap,
                                          uint8_t* d_bitmap, uint8_t* h_codes, hipStream_t stream) {
   g_tiling_used = 0;
+  g_arg_cap_used = 0;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
@@ -856,6 +861,7 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
     (void)xec_scan_stripes(h_bitmap, S, k, m, nullptr, items, xec::kArgItems, &n, &failures);
     rotate_for(items, n);
     g_tiling_used = XEC_TILING_ARG_LIST;
+    g_arg_cap_used = (int)xec::arg_items_capacity(n);
     return xec::launch_decode(d_data, d_parity, nullptr, g, ls, xec::kDecodeArgListTiles, stream,
                               n, items) == hipSuccess
                ? verdict
@@ -1119,6 +1125,32 @@ const char* xec_status_string(xec_status s) {
 #define XEC_SRC_ID "unknown"
 #endif
 // "src:<id>": the hash of the library's sources (erasure-code-benchmark_amd/Makefile)
+xec_status xec_peer_link(int device, int peer, xec_peer_link_info* out) {
+  int n = 0;
+  if (out == nullptr) return XEC_INVALID_COUNTS;
+  if (hipGetDeviceCount(&n) != hipSuccess) return XEC_DEVICE_ERROR;
+  if (device < 0 || peer < 0 || device >= n || peer >= n) return XEC_INVALID_COUNTS;
+  xec_peer_link_info r{1, -1, -1};
+  if (device != peer) {
+    if (hipDeviceCanAccessPeer(&r.can_access_peer, device, peer) != hipSuccess)
+      return XEC_DEVICE_ERROR;
+    uint32_t type = 0, hops = 0;
+    // A pair the runtime knows no link for reports an error: that is "none",
+    // not a failure of this call.  The error is ours to clear -- unless one
+    // of the caller's was pending, which stays where it was (DESIGN.md §7,
+    // the thread's error state).
+    const bool clean = hipPeekAtLastError() == hipSuccess;
+    if (hipExtGetLinkTypeAndHopCount(device, peer, &type, &hops) == hipSuccess) {
+      r.link_type = (int)type;
+      r.hop_count = (int)hops;
+    } else if (clean) {
+      (void)hipGetLastError();
+    }
+  }
+  *out = r;
+  return XEC_SUCCESS;
+}
+
 const char* xec_build_info(void) { return "xec-hip gfx950 src:" XEC_SRC_ID " " __DATE__ " " __TIME__; }
 
 }  // extern "C"

@@ -321,14 +321,15 @@ __global__ __launch_bounds__(T) void decode_list_kernel(uint8_t* data,
   }
 }
 
-// The same with the list in the kernel arguments (at most kArgItems entries;
-// the item is a scalar load from the kernarg segment): small decodes then
-// copy nothing to the device (a <= 8 KiB H2D copy runs as a blit kernel of its
-// own, 3.7-4.4 us, profiles/r02o, r02l).
-template <int NM, int U, bool NT, int T>
+// The same with the list in the kernel arguments (at most CAP entries, CAP
+// one of 64 / 256 / 1024, xec_kernels.h arg_items_capacity; the item is a
+// scalar load from the kernarg segment): small decodes then copy nothing to
+// the device (a <= 8 KiB H2D copy runs as a blit kernel of its own,
+// 3.7-4.4 us, profiles/r02o, r02l).
+template <int NM, int U, bool NT, int T, uint32_t CAP>
 __global__ __launch_bounds__(T) void decode_arglist_kernel(uint8_t* data,
                                                            const uint8_t* __restrict__ parity,
-                                                           Geometry g, ArgItems items) {
+                                                           Geometry g, ArgItems<CAP> items) {
   for (uint64_t t0 = blockIdx.x; t0 < g.total_tiles; t0 += gridDim.x) {
     const uint64_t t = g.total_tiles - 1 - t0;
     rebuild_item<NM, U, NT, T>(data, parity, items.v[t / g.tiles_per_block],
@@ -447,9 +448,10 @@ __global__ __launch_bounds__(256) void erase_kernel(uint8_t* data, uint8_t* pari
 // gather: the host pipeline's rebuilt small blocks into one contiguous run
 // (csrc/xec_pipeline.cpp: one D2H copy instead of one per block)
 // ---------------------------------------------------------------------------
+template <uint32_t CAP>
 __global__ __launch_bounds__(256) void gather_kernel(const uint8_t* __restrict__ data,
                                                      uint8_t* __restrict__ out, uint64_t k,
-                                                     uint64_t bs, uint32_t n, ArgItems items) {
+                                                     uint64_t bs, uint32_t n, ArgItems<CAP> items) {
   for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
     const uint32_t item = items.v[g];
     const uint8_t* src = data + ((uint64_t)(item >> 8) * k + (item & 0xFFu)) * bs;
@@ -491,17 +493,43 @@ hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t g
                 static_cast<uint8_t*>(p), g);
 }
 
+// The first n of h_items in an ArgItems<CAP>, the rest zero (the kernel never
+// reads past n; zeroed so a launch's arguments depend on the list alone).
+template <uint32_t CAP>
+ArgItems<CAP> arg_items(const uint32_t* h_items, uint64_t n) {
+  ArgItems<CAP> a;
+  std::memcpy(a.v, h_items, n * sizeof(uint32_t));
+  std::memset(a.v + n, 0, (CAP - n) * sizeof(uint32_t));
+  return a;
+}
+
+struct ArgList {
+  const uint32_t* items;  // host memory, read at launch
+  uint64_t n;             // <= kArgItems
+};
+
 template <int NM, int U, bool NT, int T>
 hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geometry& g,
                            int tiling, uint32_t grid, uint32_t lds, hipStream_t s,
-                           const ArgItems* args) {
+                           const ArgList& al) {
   uint8_t* dd = static_cast<uint8_t*>(d);
   const uint8_t* pp = static_cast<const uint8_t*>(p);
   const uint32_t* list = reinterpret_cast<const uint32_t*>(bm);
   if (tiling == kDecodeDevListTiles)
     return launch(decode_devlist_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
-  if (tiling == kDecodeArgListTiles)
-    return launch(decode_arglist_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, g, *args);
+  if (tiling == kDecodeArgListTiles) {
+    switch (arg_items_capacity(al.n)) {
+      case 64:
+        return launch(decode_arglist_kernel<NM, U, NT, T, 64>, grid, T, lds, s, dd, pp, g,
+                      arg_items<64>(al.items, al.n));
+      case 256:
+        return launch(decode_arglist_kernel<NM, U, NT, T, 256>, grid, T, lds, s, dd, pp, g,
+                      arg_items<256>(al.items, al.n));
+      default:
+        return launch(decode_arglist_kernel<NM, U, NT, T, 1024>, grid, T, lds, s, dd, pp, g,
+                      arg_items<1024>(al.items, al.n));
+    }
+  }
   if (tiling == kDecodeListTiles)
     return launch(decode_list_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
   if (tiling == kDecodeClassTiles)
@@ -531,7 +559,7 @@ hipError_t enc_nm(const void* d, void* p, const Geometry& g, uint32_t grid, uint
 
 template <int U, bool NT, int T>
 hipError_t dec_nm(void* d, const void* p, const uint8_t* bm, const Geometry& g, int tiling,
-                  uint32_t grid, uint32_t lds, hipStream_t s, const ArgItems* a) {
+                  uint32_t grid, uint32_t lds, hipStream_t s, const ArgList& a) {
   XEC_NM_SWITCH(g.nm,
                 return (launch_decode_t<NM, U, NT, T>(d, p, bm, g, tiling, grid, lds, s, a)))
 }
@@ -545,7 +573,7 @@ hipError_t enc_u(const void* d, void* p, const Geometry& g, int unroll, uint32_t
 
 template <bool NT, int T>
 hipError_t dec_u(void* d, const void* p, const uint8_t* bm, const Geometry& g, int tiling,
-                 int unroll, uint32_t grid, uint32_t lds, hipStream_t s, const ArgItems* a) {
+                 int unroll, uint32_t grid, uint32_t lds, hipStream_t s, const ArgList& a) {
   return unroll == 2 ? dec_nm<2, NT, T>(d, p, bm, g, tiling, grid, lds, s, a)
                      : dec_nm<1, NT, T>(d, p, bm, g, tiling, grid, lds, s, a);
 }
@@ -580,12 +608,9 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
       tiling == kDecodeDevListTiles)
     g.total_tiles = n_items * g.tiles_per_block;
   if (g.total_tiles == 0) return hipSuccess;
-  ArgItems args;
-  if (tiling == kDecodeArgListTiles) {
-    if (n_items > kArgItems || h_items == nullptr) return hipErrorInvalidValue;
-    std::memcpy(args.v, h_items, n_items * sizeof(uint32_t));
-  }
-  const ArgItems* a = tiling == kDecodeArgListTiles ? &args : nullptr;
+  if (tiling == kDecodeArgListTiles && (n_items > kArgItems || h_items == nullptr))
+    return hipErrorInvalidValue;
+  const ArgList a{h_items, n_items};
   const uint32_t grid = grid_for(g.total_tiles, ls.max_grid, ls.threads);
   const uint32_t lds = ls.lds_bytes;
   if (ls.threads == 256)
@@ -625,10 +650,20 @@ hipError_t launch_gather(const void* d_data, void* d_out, uint64_t k, uint64_t b
   if (n == 0) return hipSuccess;
   if (n > kArgItems || k == 0 || k > 256 || bs % 16 != 0 || h_items == nullptr)
     return hipErrorInvalidValue;
-  ArgItems a;
-  std::memcpy(a.v, h_items, n * sizeof(uint32_t));
-  return launch(gather_kernel, grid_for(n, 0, 256), 256, 0, s, static_cast<const uint8_t*>(d_data),
-                static_cast<uint8_t*>(d_out), k, bs, (uint32_t)n, a);
+  const uint8_t* src = static_cast<const uint8_t*>(d_data);
+  uint8_t* dst = static_cast<uint8_t*>(d_out);
+  const uint32_t grid = grid_for(n, 0, 256);
+  switch (arg_items_capacity(n)) {
+    case 64:
+      return launch(gather_kernel<64>, grid, 256, 0, s, src, dst, k, bs, (uint32_t)n,
+                    arg_items<64>(h_items, n));
+    case 256:
+      return launch(gather_kernel<256>, grid, 256, 0, s, src, dst, k, bs, (uint32_t)n,
+                    arg_items<256>(h_items, n));
+    default:
+      return launch(gather_kernel<1024>, grid, 256, 0, s, src, dst, k, bs, (uint32_t)n,
+                    arg_items<1024>(h_items, n));
+  }
 }
 
 hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_base,

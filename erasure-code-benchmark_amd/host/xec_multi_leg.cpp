@@ -38,6 +38,7 @@
 #include <string>
 #include <vector>
 
+#include "peer_path.hpp"
 #include "xec.h"
 #include "xec_plugin_options.hpp"
 #include "xorec_hip_multi_bm.hpp"
@@ -179,10 +180,28 @@ bool exchange(LegBench& bench, const Args& a, size_t S_total, std::string& js) {
     }
   }
   release();
-  // stripes that cross a link: every shard's range except the root's own
+  // stripes that cross a link: every shard's range except the root's own; and
+  // how each shard's copies went (peer DMA, staged by the runtime, or local)
   size_t remote = 0;
-  for (size_t i = 0; i < bench.num_shards(); ++i)
+  std::vector<const char*> paths;
+  std::string access = "[";
+  for (size_t i = 0; i < bench.num_shards(); ++i) {
     if (bench.shard_device(i) != a.root) remote += bench.shard_count(i);
+    const xec_hip::PeerAccess pa = bench.shard_peer_access(i);
+    const char* name = pa == xec_hip::PeerAccess::kEnabled      ? "enabled"
+                       : pa == xec_hip::PeerAccess::kStaged     ? "staged"
+                       : pa == xec_hip::PeerAccess::kSameDevice ? "same-device"
+                                                                : "error";
+    access += std::string(i ? "," : "") + "\"" + name + "\"";
+    xec_peer_link_info li{0, -1, -1};
+    const bool known = xec_peer_link(bench.shard_device(i), a.root, &li) == XEC_SUCCESS;
+    paths.push_back(pa == xec_hip::PeerAccess::kStaged
+                        ? "staged"
+                        : xec_hip::peer_path_label(bench.shard_device(i) == a.root,
+                                                   known && li.can_access_peer, li.link_type));
+  }
+  access += "]";
+  const char* path = xec_hip::scatter_path_label(paths.data(), paths.size());
   const double sc = t_sc.empty() ? 0 : *std::min_element(t_sc.begin(), t_sc.end());
   const double ga = t_ga.empty() ? 0 : *std::min_element(t_ga.begin(), t_ga.end());
   js += ",\"scatter\":{\"root\":" + std::to_string(a.root) +
@@ -192,11 +211,14 @@ bool exchange(LegBench& bench, const Args& a, size_t S_total, std::string& js) {
         (sc > 0 ? jnum(remote * a.k * a.bs / sc / 1e9, 1) : std::string("null")) +
         ",\"root_ingress_GBps\":" +
         (ga > 0 ? jnum(remote * a.m * a.bs / ga / 1e9, 1) : std::string("null")) +
-        ",\"reps\":" + std::to_string(a.scatter_reps) +
+        ",\"reps\":" + std::to_string(a.scatter_reps) + ",\"path\":\"" + path + "\"" +
+        ",\"peer_access_by_shard\":" + access +
         ",\"gathered_parity_bit_exact_vs_root_encode\":" + (exact ? "true" : "false") +
         (ok ? "" : ",\"error\":\"a HIP call failed during the exchange\"") +
-        ",\"note\":\"batch starts in the root's HBM; hipMemcpyPeerAsync per shard (xGMI "
-        "between GPUs, a device copy where shard and root share one); best of reps\"}";
+        ",\"note\":\"batch starts in the root's HBM; hipMemcpyPeerAsync per shard: peer DMA "
+        "where the pair has peer access (path xgmi-p2p over xGMI), staged by the runtime where "
+        "it has not (path staged), a device copy where shard and root share one; best of "
+        "reps\"}";
   return ok && exact;
 }
 
@@ -250,12 +272,23 @@ int main(int argc, char** argv) {
       js += (i ? "," : "") + std::to_string(bus);
     }
     js += "],\"peer_access_to_root\":[";
+    std::string topo = ",\"topology\":{\"root\":" + std::to_string(a.root) + ",\"pairs\":[";
+    std::vector<const char*> labels;
     for (size_t i = 0; i < n; ++i) {
-      int can = a.devices[i] == a.root ? 1 : 0;
-      if (!can) (void)hipDeviceCanAccessPeer(&can, a.devices[i], a.root);
-      js += (i ? "," : "") + std::to_string(can);
+      xec_peer_link_info li{0, -1, -1};
+      const bool known = xec_peer_link(a.devices[i], a.root, &li) == XEC_SUCCESS;
+      const bool same = a.devices[i] == a.root;
+      js += (i ? "," : "") + std::to_string(known && li.can_access_peer ? 1 : 0);
+      labels.push_back(xec_hip::peer_path_label(same, known && li.can_access_peer, li.link_type));
+      topo += std::string(i ? "," : "") + "{\"device\":" + std::to_string(a.devices[i]) +
+              ",\"peer\":" + std::to_string(a.root) +
+              ",\"can_access_peer\":" + (known ? std::to_string(li.can_access_peer) : "null") +
+              ",\"link_type\":\"" + xec_hip::link_type_name(li.link_type) + "\"" +
+              ",\"hop_count\":" + (li.hop_count >= 0 ? std::to_string(li.hop_count) : "null") +
+              ",\"path\":\"" + labels.back() + "\"}";
     }
-    js += "]";
+    js += "]" + topo + "],\"path\":\"" + xec_hip::scatter_path_label(labels.data(), labels.size()) +
+          "\",\"source\":\"hipDeviceCanAccessPeer + hipExtGetLinkTypeAndHopCount (xec_peer_link)\"}";
     for (int i = 0; i < a.warmup; ++i) {
       bench.setup();
       (void)bench.encode();

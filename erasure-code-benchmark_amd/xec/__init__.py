@@ -6,7 +6,8 @@ multi-GPU partitioning helpers; it never computes parity itself.
 """
 from ._lib import EXPORTED, LIB_PATH, Status, XecLibraryError, lib
 from .codec import (DECODE_KERNELS, Pipeline, build_info, check_args, check_bitmap, decode,
-                    decode_device, decode_device_list, decode_per_stripe, decode_tiling_used,
+                    decode_arg_capacity_used, decode_device, decode_device_list,
+                    decode_per_stripe, decode_tiling_used,
                     device_list_bytes, encode, erase,
                     fill_splitmix64, init,
                     select_lost_blocks, set_decode_tiling, set_launch, set_occupancy,
@@ -16,7 +17,8 @@ from .partition import stripe_range
 
 __all__ = [
     "DECODE_KERNELS", "EXPORTED", "LIB_PATH", "Pipeline", "Status", "XecLibraryError", "lib",
-    "build_info", "check_args", "check_bitmap", "decode", "decode_device", "decode_device_list",
+    "build_info", "check_args", "check_bitmap", "decode", "decode_arg_capacity_used",
+    "decode_device", "decode_device_list",
     "decode_per_stripe", "decode_tiling_used", "device_list_bytes",
     "encode", "erase", "fill_splitmix64", "init", "select_lost_blocks", "set_decode_tiling",
     "set_launch",

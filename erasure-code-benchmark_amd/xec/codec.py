@@ -164,6 +164,12 @@ def decode_tiling_used() -> int:
     return int(lib().xec_decode_tiling_used())
 
 
+def decode_arg_capacity_used() -> int:
+    """xec_decode_arg_capacity_used: after a kernel-argument list decode, the
+    capacity its arguments carried (64, 256 or 1024 entries); else 0."""
+    return int(lib().xec_decode_arg_capacity_used())
+
+
 def status_string(st: int) -> str:
     return lib().xec_status_string(int(st)).decode()
 

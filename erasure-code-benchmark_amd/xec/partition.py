@@ -15,3 +15,20 @@ def stripe_range(S: int, rank: int, world: int) -> tuple[int, int]:
     base, extra = divmod(S, world)
     start = rank * base + min(rank, extra)
     return start, start + base + (1 if rank < extra else 0)
+
+
+#: GPUs of one node in BASELINE.json configs[4] (config 5)
+CONFIG5_GPUS = 8
+
+
+def config5_devices(visible: int, gpus: int = CONFIG5_GPUS) -> list[int]:
+    """The device list config 5's one-process tests run:
+    the distinct devices 0 .. min(visible, gpus) - 1 whenever more than one GPU
+    is visible, so the peer copies cross real links; on a one-GPU box device 0
+    repeated `gpus` times, so the full shape still runs (its copies are device
+    copies)."""
+    if visible < 1:
+        raise ValueError("no visible GPU")
+    if visible >= 2:
+        return list(range(min(visible, gpus)))
+    return [0] * gpus

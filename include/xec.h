@@ -296,6 +296,10 @@ enum {
   XEC_TILING_ARG_LIST = 4  /* decode_arglist_kernel: the same, list in the kernel arguments */
 };
 int xec_decode_tiling_used(void);
+/* With XEC_TILING_ARG_LIST: how many entries the kernel-argument list of that
+ * launch could hold -- 64, 256 or 1024, the smallest capacity that holds the
+ * list, so a short list ships short kernel arguments; 0 for any other tiling. */
+int xec_decode_arg_capacity_used(void);
 
 /* ---- host-in / host-out pipeline --------------------
  * The MI355X analogue of the reference's GPU-memory / unified-memory variants
@@ -338,6 +342,27 @@ const char* xec_status_string(xec_status s);
 
 /* Build identification, e.g. "xec-hip gfx950 <date>". */
 const char* xec_build_info(void);
+
+/* ---- node topology (diagnostics; no reference counterpart) ----------------
+ * The reference drives one GPU (xorec_gpu_cmp.cu:7-16).  Config 5 scatters
+ * stripe ranges from a root GPU to its peers; how those bytes travel depends
+ * on the pair, so the multi-GPU runs record it:
+ *   can_access_peer  hipDeviceCanAccessPeer(device, peer): 1 when `device`
+ *                    can map `peer`'s memory (direct peer DMA), else 0 --
+ *                    a copy between them is staged by the runtime;
+ *   link_type        hipExtGetLinkTypeAndHopCount: the HSA link type
+ *                    (XEC_LINK_PCIE 2, XEC_LINK_XGMI 4, ...), -1 when the
+ *                    runtime reports none (device == peer, or no link);
+ *   hop_count        hops of that link, -1 likewise.
+ * XEC_INVALID_COUNTS for a device id outside 0..count-1, XEC_DEVICE_ERROR
+ * when the runtime fails; *out is written only on success. */
+enum { XEC_LINK_PCIE = 2, XEC_LINK_XGMI = 4 };
+typedef struct {
+  int can_access_peer;
+  int link_type;
+  int hop_count;
+} xec_peer_link_info;
+xec_status xec_peer_link(int device, int peer, xec_peer_link_info* out);
 
 #ifdef __cplusplus
 }

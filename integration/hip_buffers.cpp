@@ -68,17 +68,18 @@ bool set_sync_mode(int mode) {
   return false;
 }
 
-bool enable_peer_access(int device, int peer) {
-  if (device == peer) return true;
+PeerAccess enable_peer_access(int device, int peer) {
+  if (device == peer) return PeerAccess::kSameDevice;
   int can = 0;
-  if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess) return false;
-  if (!can) return true;  // the runtime stages such copies itself
+  if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess) return PeerAccess::kError;
+  if (!can) return PeerAccess::kStaged;  // copies still work: the runtime stages them
   const int prev = current_device();
-  if (hipSetDevice(device) != hipSuccess) return false;
+  if (hipSetDevice(device) != hipSuccess) return PeerAccess::kError;
   const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
   if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();  // ours: clear it
   if (prev >= 0) (void)hipSetDevice(prev);
-  return e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+  return e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled ? PeerAccess::kEnabled
+                                                                 : PeerAccess::kError;
 }
 
 bool copy_peer(void* dst, int dst_device, const void* src, int src_device, size_t bytes,

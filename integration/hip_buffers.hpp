@@ -46,8 +46,17 @@ bool set_device(int device);
 bool set_sync_mode(int mode);
 
 // `device` gets access to `peer`'s memory where the pair supports it (an
-// access already enabled is fine); true unless a runtime call failed.
-bool enable_peer_access(int device, int peer);
+// access already enabled is fine).  The result says which (VERDICT r05 item
+// 2): a pair without peer access still copies -- hipMemcpyPeerAsync stages the
+// bytes -- but that is not peer DMA, and the caller reports it as "staged"
+// (peer_path.hpp), never as an xGMI transfer.
+enum class PeerAccess : int {
+  kError = -1,      // a runtime call failed
+  kSameDevice = 0,  // device == peer: nothing to enable
+  kEnabled = 1,     // peer access on (now, or already)
+  kStaged = 2,      // the pair cannot access each other: copies are staged
+};
+PeerAccess enable_peer_access(int device, int peer);
 
 // Stream-ordered copy between two devices' memory (xGMI DMA between GPUs, a
 // device copy when both are the same device); true on success.

@@ -309,10 +309,17 @@ bool XorecBenchmarkHipMulti::check_for_corruption() const noexcept {
   return ok && std::all_of(bad.begin(), bad.end(), [](uint32_t b) { return b == 0; });
 }
 
-bool XorecBenchmarkHipMulti::enable_peers(int root) const noexcept {
-  for (const Shard& s : m_shards)
-    if (!xec_hip::enable_peer_access(s.device, root)) return false;
-  return true;
+// Each shard's device gets access to the root's memory where the pair allows
+// it; a pair without peer access still exchanges (the runtime stages the
+// copies) and is recorded as such, so the caller can tell peer DMA from a
+// staged copy.  False only if a runtime call failed.
+bool XorecBenchmarkHipMulti::enable_peers(int root) noexcept {
+  bool ok = true;
+  for (Shard& s : m_shards) {
+    s.peer = xec_hip::enable_peer_access(s.device, root);
+    ok = ok && s.peer != xec_hip::PeerAccess::kError;
+  }
+  return ok;
 }
 
 int XorecBenchmarkHipMulti::scatter_from(const uint8_t* d_root_data, int root) noexcept {

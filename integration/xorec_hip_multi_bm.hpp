@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "abstract_bm.hpp"
+#include "hip_buffers.hpp"
 #include "xec.h"
 #include "xec_plugin_options.hpp"
 
@@ -56,6 +57,12 @@ public:
   // independent.
   int scatter_from(const uint8_t* d_root_data, int root) noexcept;
   int gather_parity_to(uint8_t* d_root_parity, int root) noexcept;
+  // How shard i's device reached the root in the last scatter_from /
+  // gather_parity_to (hip_buffers.hpp PeerAccess): kEnabled = peer DMA,
+  // kStaged = the pair has no peer access and the runtime staged the copies
+  // (reported as "staged", peer_path.hpp), kSameDevice = a device copy;
+  // kError before any exchange.
+  xec_hip::PeerAccess shard_peer_access(size_t i) const noexcept { return m_shards[i].peer; }
 
   // Shards and diagnostics for the harness and tests.
   size_t num_shards() const noexcept { return m_shards.size(); }
@@ -82,6 +89,7 @@ private:
     DevBuf d_erase{nullptr, nullptr};   ///< device copy of the erasure bitmap slice
     DevBuf d_bad{nullptr, nullptr};     ///< device count of invalid blocks
     DevBuf h_stage{nullptr, nullptr};   ///< pinned copy of the range (host payload / check)
+    xec_hip::PeerAccess peer = xec_hip::PeerAccess::kError;  ///< to the last exchange's root
   };
 
   // Runs fn(shard) on every shard with its device current, then waits for
@@ -89,7 +97,7 @@ private:
   // device is restored.
   template <typename F>
   bool each(F&& fn) const noexcept;
-  bool enable_peers(int root) const noexcept;
+  bool enable_peers(int root) noexcept;
   void destroy_streams() noexcept;
 
   XecPluginOptions m_opt;

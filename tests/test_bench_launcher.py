@@ -143,3 +143,52 @@ def test_world1_process_group_rehearsal():
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert out["n_gpus"] == 1 and out["dist"]["ranks_seen"] == 1
     assert out["scatter"]["bit_exact"] is True
+
+
+@pytest.mark.parametrize("stub,path", [("xgmi", "xgmi-p2p"), ("staged", "staged")])
+def test_topology_record_in_the_line(stub, path):
+    """the N > 1 line records, per root -> peer pair, peer
+    access, link type and hops, and labels the scatter "xgmi-p2p" or "staged"
+    from that record -- here from a stubbed topology (XEC_TOPOLOGY_STUB), since
+    the CPU has no runtime to ask."""
+    import os
+    env = dict(os.environ, XEC_TOPOLOGY_STUB=stub)
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--rehearse-cpu",
+                        "--dist-backend", "gloo", "--workload", "8,2,4096,5", "--steps", "2",
+                        "--warmup", "1", "--multi-devices", "none"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    topo = out["topology"]
+    assert topo["root"] == 0 and [q["device"] for q in topo["pairs"]] == [0, 1, 2, 3]
+    assert topo["pairs"][0]["path"] == "local"
+    assert all(q["path"] == path for q in topo["pairs"][1:])
+    assert topo["path"] == path and "STUB" in topo["source"]
+    assert out["scatter"]["path"] == path
+
+
+def test_topology_record_needs_a_runtime_or_a_stub():
+    import os
+    env = {k: v for k, v in os.environ.items() if k != "XEC_TOPOLOGY_STUB"}
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--rehearse-cpu",
+                        "--dist-backend", "gloo", "--workload", "8,2,4096,5", "--steps", "2",
+                        "--warmup", "1", "--multi-devices", "none"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert "skipped" in out["topology"] and out["scatter"]["path"] == "unknown"
+
+
+@pytest.mark.parametrize("stub,path", [("xgmi", "xgmi-p2p"), ("staged", "staged")])
+def test_multi_leg_stand_in_topology(stub, path):
+    """The multi_device leg's record (host/xec_multi_leg.cpp: "topology" and the
+    scatter's "path"), from the CPU stand-in over a stubbed 4-GPU node."""
+    import os
+    env = dict(os.environ, XEC_TOPOLOGY_STUB=stub)
+    p = subprocess.run([sys.executable, str(ROOT / "tools" / "cpu_rehearsal.py"), "multi-leg",
+                        "--devices", "0,1,2,3", "--stripes-per-device", "2", "--data", "4",
+                        "--block", "4096"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["topology"]["path"] == path and out["scatter"]["path"] == path
+    assert [q["path"] for q in out["topology"]["pairs"]] == ["local"] + [path] * 3

@@ -1,18 +1,26 @@
 """Config 5 (BASELINE.json configs[4]: k=16+1, 1 MiB shards, stripe batches
-partitioned over the 8 GPUs of one node) at its FULL shape, in every GPU run
-(VERDICT r04 item 1).
+partitioned over the 8 GPUs of one node) at its FULL per-device shape, in every
+GPU run, over distinct devices wherever the box has them
+(VERDICT r05 item 1).
 
 bin/xec_multi_leg is the exact program bench.py's multi-device leg runs on the
-driver's 8-GPU node (host/xec_multi_leg.cpp).  On a one-GPU box the device
-list repeats device 0 eight times: eight shards of 256 stripes, each with its
-own stream and 4 GiB of data in HBM, plus the root's 34 GiB batch that the
-exchange scatters from (copies past the 4 GiB offset) and gathers parity back
-to.  What is asserted is what the 8-GPU run depends on:
+driver's 8-GPU node (host/xec_multi_leg.cpp).  Two device lists
+(xec.partition.config5_devices):
+  * device 0 repeated eight times -- always: eight shards of 256 stripes, each
+    with its own stream and 4 GiB of data in HBM, plus the root's 34 GiB batch
+    that the exchange scatters from (copies past the 4 GiB offset) and gathers
+    parity back to;
+  * devices 0 .. min(n, 8) - 1 when n >= 2 GPUs are visible: the same shape per
+    device, so the scatter / gather cross real links before the driver's
+    scaling run does (skipped, with the reason, on a one-GPU box).
+What is asserted is what the 8-GPU run depends on:
   * every timed iteration's decode rebuilt every lost block (validate_block,
     /root/reference/src/utils/utils.cpp:72-97, on every shard),
   * the codec returned success on every shard,
   * the gathered parity equals the root's own encode of the whole batch,
-    byte for byte (stripe independence, src/algorithms/xorec_bm.cpp:30).
+    byte for byte (stripe independence, src/algorithms/xorec_bm.cpp:30),
+  * over distinct devices: every pair reports peer access, and the copies went
+    by peer DMA (not staged by the runtime).
 """
 from __future__ import annotations
 
@@ -22,31 +30,69 @@ import subprocess
 import pytest
 
 from conftest import PKG_DIR
+from xec.partition import config5_devices
 
 LEG = PKG_DIR / "bin" / "xec_multi_leg"
 
 
-@pytest.mark.gpu
-def test_config5_full_shape_one_process_leg():
+def _visible() -> int:
+    import torch
+    return torch.cuda.device_count()  # counts devices without initialising one
+
+
+def _run_leg(devices, timeout=600):
     assert LEG.exists(), "build with make -C erasure-code-benchmark_amd"
-    cmd = [str(LEG), "--devices", ",".join(["0"] * 8), "--stripes-per-device", "256",
+    cmd = [str(LEG), "--devices", ",".join(map(str, devices)), "--stripes-per-device", "256",
            "--data", "16", "--parity", "1", "--block", "1M", "--iterations", "3",
            "--warmup", "1", "--scatter-reps", "1"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, p.stdout + p.stderr
     out = json.loads(lines[-1])
     assert p.returncode == 0, out
     assert "error" not in out, out
-    assert out["stripes_total"] == 2048 and out["stripes_per_device"] == 256
-    assert out["devices"] == [0] * 8 and out["k"] == 16 and out["m"] == 1
+    n = len(devices)
+    assert out["stripes_total"] == 256 * n and out["stripes_per_device"] == 256
+    assert out["devices"] == list(devices) and out["k"] == 16 and out["m"] == 1
     assert out["block_bytes"] == 1 << 20
     assert out["codec_status"] == 0
     assert out["corrupted_iterations"] == 0
     assert out["bit_exact"] is True
     # one lost block per stripe, drawn over all 17 blocks: ~16/17 of them data
-    assert 0 < out["lost_data_blocks_per_iteration"] <= 2048
+    assert 0 < out["lost_data_blocks_per_iteration"] <= 256 * n
     sc = out["scatter"]
     assert "error" not in sc, sc
     assert sc["gathered_parity_bit_exact_vs_root_encode"] is True
     assert out["encode_GBps"] > 0 and out["decode_GBps"] > 0
+    topo = out["topology"]
+    assert topo["root"] == devices[0] and len(topo["pairs"]) == n
+    return out
+
+
+@pytest.mark.gpu
+def test_config5_full_shape_one_gpu():
+    """Device 0 eight times: the full shape on any box."""
+    out = _run_leg(config5_devices(1))
+    assert out["distinct_devices"] == 1
+    assert out["topology"]["path"] == "local" and out["scatter"]["path"] == "local"
+
+
+@pytest.mark.gpu
+def test_config5_distinct_devices():
+    """Devices 0 .. min(n, 8) - 1, each with config 5's 256 stripes: the
+    scatter and gather cross the links between GPUs."""
+    n = _visible()
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: config 5 over distinct devices needs 2 or more "
+                    "(the driver's 8-GPU node runs it)")
+    devices = config5_devices(n)
+    out = _run_leg(devices, timeout=900)
+    assert out["distinct_devices"] == len(devices)
+    pairs = out["topology"]["pairs"]
+    assert all(p["can_access_peer"] == 1 for p in pairs), pairs
+    assert all(p["path"] != "staged" for p in pairs), pairs
+    assert out["peer_access_to_root"] == [1] * len(devices)
+    sc = out["scatter"]
+    assert sc["path"] != "staged", sc
+    assert sc["peer_access_by_shard"][0] == "same-device"
+    assert all(a == "enabled" for a in sc["peer_access_by_shard"][1:]), sc

@@ -364,6 +364,34 @@ def test_golden_decode_fixtures_each_tiling(gpu, oracle, known_answers, tiling):
         gpu.set_decode_tiling(0)
 
 
+@pytest.mark.parametrize("S,k,m,bs,lost", [
+    (1024, 8, 1, 1024, 1), (1024, 8, 1, 1024, 64),        # capacity 64, at its edge
+    (1024, 8, 1, 1024, 65), (1024, 8, 1, 1024, 256),      # 256
+    (1024, 8, 1, 1024, 257), (1024, 8, 1, 1024, 1024),    # 1024, the largest
+    (300, 16, 4, 2048, 200), (300, 16, 4, 2048, 900),     # several per stripe, m = 4
+    (64, 32, 1, 4352, 64),                                # ragged tail tile, 32 members
+])
+def test_decode_arg_list_capacities_bit_exact(gpu, oracle, S, k, m, bs, lost):
+    """The kernel-argument work list ships the smallest of 64 / 256 / 1024
+    entries that holds it (xec_kernels.h arg_items_capacity):
+    every capacity, on both sides of each boundary, rebuilds bit-exactly."""
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    bm = np.ones((S, k + m), np.uint8)
+    rng = np.random.default_rng(S + lost)
+    classes = [(c, j) for c in range(S) for j in range(m)]
+    for idx in rng.choice(len(classes), size=lost, replace=False):
+        c, j = classes[idx]
+        bm[c, j + m * int(rng.integers(k // m))] = 0
+    assert gpu.set_decode_tiling(3) == gpu.Status.SUCCESS
+    try:
+        erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+        assert gpu.decode_tiling_used() == 4
+        want = 64 if lost <= 64 else 256 if lost <= 256 else 1024
+        assert gpu.decode_arg_capacity_used() == want
+    finally:
+        gpu.set_decode_tiling(0)
+
+
 def test_decode_tiling_argument_range(gpu):
     assert gpu.set_decode_tiling(4) == gpu.Status.INVALID_SIZE
     assert gpu.set_decode_tiling(-1) == gpu.Status.INVALID_SIZE

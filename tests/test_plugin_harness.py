@@ -183,6 +183,22 @@ def test_multi_device_scatter_gather():
 
 
 @pytest.mark.gpu
+def test_multi_device_scatter_gather_distinct_gpus():
+    """The same exchange over the distinct devices 0 .. min(n, 8) - 1 (VERDICT
+    r05 item 1): peer copies between GPUs, 4.5 GiB ones included, and every
+    remote shard reached the root by peer access, not a staged copy
+    (multi_scatter --distinct).  Skipped on a one-GPU box."""
+    import torch
+    n = torch.cuda.device_count()  # counts devices without initialising one
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: peer copies between distinct GPUs need 2 or more")
+    assert MULTI_SCATTER.exists(), "build with make -C tests/host"
+    p = subprocess.run([str(MULTI_SCATTER), "--distinct"], capture_output=True, text=True,
+                       timeout=600)
+    assert p.returncode == 0 and "multi_scatter ok" in p.stdout, p.stdout + p.stderr
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("prog,ok", [("asan_multi_equiv", "multi_equiv ok"),
                                      ("asan_multi_scatter", "multi_scatter ok"),
                                      ("asan_abi", "abi_asan ok")])

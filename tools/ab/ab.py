@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--rotations", default="",
                     help="comma list of xec_set_rotation values to cross with --libs "
                          "(-1 none, 0 automatic, > 0 KiB per stripe); default: each lib's own")
+    ap.add_argument("--tilings", default="",
+                    help="comma list of xec_set_decode_tiling values to cross with --libs in "
+                         "the same process (0 automatic, 1 stripe, 2 class, 3 work list)")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the identical-results check (diagnostic builds that store elsewhere)")
     ap.add_argument("--out", default="")
@@ -83,6 +86,10 @@ def main():
             for v in args.variants.split(";"):
                 u, t, o = (int(x) for x in v.split(","))
                 libs[f"{n}@u{u}t{t}o{o}"] = (L, (u, t, o))
+            continue
+        if args.tilings:
+            for t in (int(x) for x in args.tilings.split(",")):
+                libs[f"{n}@t{t}"] = (L, ("til", t))
             continue
         if args.rotations:
             for r in (int(x) for x in args.rotations.split(",")):
@@ -117,7 +124,9 @@ def main():
     # every build must produce the same parity and the same rebuilt data
     ref = None
     def use(L, o):
-        if isinstance(o, tuple) and o[0] == "rot":
+        if isinstance(o, tuple) and o[0] == "til":
+            assert L.xec_set_decode_tiling(o[1]) == 0
+        elif isinstance(o, tuple) and o[0] == "rot":
             assert L.xec_set_rotation(o[1]) == 0
         elif isinstance(o, tuple):
             assert L.xec_set_launch(o[0], 0, 0, o[1]) == 0

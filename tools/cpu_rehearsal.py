@@ -148,12 +148,18 @@ def multi_leg_main(argv):
         gathered[a0 * m * bs_r:a1 * m * bs_r] = par  # "gather"
     t = time.perf_counter() - t0
     exact = bool(torch.equal(gathered, ref))
+    import os
+    from xec import topology
+    topo = (topology.record(devices[0], devices) if os.environ.get("XEC_TOPOLOGY_STUB")
+            else {"skipped": "CPU rehearsal: no runtime to ask (set XEC_TOPOLOGY_STUB)"})
     out = {"plugin": "CPU REHEARSAL stand-in (tools/cpu_rehearsal.py): not a measurement",
            "rehearsal": True, "devices": devices, "k": k, "m": m, "block_bytes": bs,
            "stripes_per_device": S_per, "stripes_total": S,
            "distinct_devices": len(set(devices)), "encode_ms": round(t * 1e3, 4),
            "decode_ms": round(t * 1e3, 4), "value_GBps": 0.0, "bit_exact": exact,
-           "scatter": {"root": devices[0], "gathered_parity_bit_exact_vs_root_encode": exact}}
+           "topology": topo,
+           "scatter": {"root": devices[0], "gathered_parity_bit_exact_vs_root_encode": exact,
+                       "path": topo.get("path", "unknown")}}
     print(json.dumps(out))
     sys.exit(0 if exact else 1)
 
