@@ -58,7 +58,7 @@ uint32_t lds_for_occupancy(int waves, int threads) {
 
 // Resident waves per SIMD that measured fastest for the default shape (one
 // wave per workgroup, one granule per lane), by class member count k/m
-// (tools/archive/sweep.py --occ; profiles/r01i, r01j: two devices, encode and decode,
+// (bf0ca45:tools/archive/sweep.py --occ; profiles/r01i, r01j: two devices, encode and decode,
 // k=4..32).  A wave keeps up to k/m KiB of loads in flight (~11 KiB at k/m =
 // 16, hipcc's rolling window; all 32 at k/m = 32); the best residency keeps
 // roughly 16-32 KiB in flight per SIMD -- 8 waves per SIMD at k/m = 16 queue
@@ -81,7 +81,7 @@ int auto_occupancy(uint64_t nm) {
 // Decode does one class reduction per lost data block of its stripe, one after
 // the other, so its work per tile is k/m x (lost blocks per stripe) loads.  At
 // one erasure per stripe that is the encode table above; with several
-// (tools/archive/sweep.py --lost, profiles/r01p: 16+2, 16+4, 16+8, 32+8, 8+2 at 2..8
+// (bf0ca45:tools/archive/sweep.py --lost, profiles/r01p: 16+2, 16+4, 16+8, 32+8, 8+2 at 2..8
 // erasures per stripe) 2 waves per SIMD measured best from 8 loads per tile
 // up (+3 to +15 % over the single-erasure choice), 4 from 4.  Only the member
 // counts those shapes cover (2, 4, 8) take this branch.
@@ -99,7 +99,7 @@ int decode_auto_occupancy(uint64_t nm, uint64_t lost_data, uint64_t S) {
 // none idle, whatever the spread of the losses.  Otherwise, stripe tiles run
 // one class reduction per lost data block of their stripe, back to back;
 // class tiles are encode's tiles, one reduction each, but a class without a
-// loss leaves its tiles idle.  Measured in one process on both (tools/archive/tiling_ab.py,
+// loss leaves its tiles idle.  Measured in one process on both (bf0ca45:tools/archive/tiling_ab.py,
 // profiles/r02a/tiling_ab.json; 16+2, 8+2 x 1 MiB, 16+4, 16+8, 32+8 x 64 KiB at
 // 1, m/2 and m losses per stripe): class tiles win once more than one block
 // per stripe AND at least half of the classes are lost (+3 to +9 % with every
@@ -148,15 +148,20 @@ void clear_own_not_ready() {
 }
 
 // hipEventQuery on a buffer's event (recorded on a stream the library owns,
-// track_stream below): 1 once the work it marks has passed, 0 not yet (or not
-// asked: a caller's error is pending, and the buffer is taken as in use), -1
-// the query failed -- a sticky device fault, which fails the call.
+// track_stream below): 1 once the work it marks has passed, 0 not yet, -1 the
+// query failed -- a sticky device fault, which fails the call.  The query is
+// asked even while an error of the caller's is pending: taking
+// every buffer as in use then made each call allocate a new one up to the
+// pool's cap and then wait on a recycled one.  On this runtime a successful
+// query leaves the pending error alone and a NotReady is not recorded
+// (profiles/r05b), so only the clearing step is skipped: the pending error is
+// the caller's, never ours to clear.
 int event_passed(hipEvent_t e) {
-  if (caller_error_pending()) return 0;
+  const bool callers = caller_error_pending();
   const hipError_t q = hipEventQuery(e);
   if (q == hipSuccess) return 1;
   if (q == hipErrorNotReady) {
-    clear_own_not_ready();
+    if (!callers) clear_own_not_ready();
     return 0;
   }
   return -1;
@@ -500,7 +505,7 @@ void upload_end(Upload& up, hipStream_t stream, bool launched) {
   up.slot = nullptr;
 }
 
-// Defaults measured on MI355X (tools/archive/sweep.py, profiles/r01_sweep_*.json):
+// Defaults measured on MI355X (bf0ca45:tools/archive/sweep.py, profiles/r01_sweep_*.json):
 // non-temporal loads and parity stores, sc1 rebuilt-block stores (every byte
 // is touched once; xec_kernels.hip kEncodeStoreAux / kDecodeStoreAux), one-wave
 // workgroups with one 1 KiB tile each, one workgroup per tile, residency
@@ -625,7 +630,7 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
 // Bitmaps from this size on are copied to the device BEFORE the host scan, so
 // the scan (~1.1 ns per stripe, 75 us for config 4's 65,536 stripes) runs
 // while the transfer does and the synchronous caller waits for
-// max(scan, copy) + kernel instead of their sum (tools/archive/scan_cost.py,
+// max(scan, copy) + kernel instead of their sum (bf0ca45:tools/archive/scan_cost.py,
 // profiles/r02b, r02c).  Smaller bitmaps keep the scan first, so a batch that
 // needs no recovery queues no device work at all.
 constexpr size_t kCopyFirstBitmapBytes = 256u << 10;
@@ -633,7 +638,7 @@ constexpr size_t kCopyFirstBitmapBytes = 256u << 10;
 // Work-list tiles are taken (automatic tiling) when at most this fraction of
 // the stripes lost a data block: then stripe and class tiles would leave most
 // of their tiles idle (sparse: 2.2x faster at 1 stripe in 9, skewed: 1.0-3.1x
-// at 1 in 5; tools/archive/tiling_ab.py --pattern, profiles/r02n).  When every stripe
+// at 1 in 5; bf0ca45:tools/archive/tiling_ab.py --pattern, profiles/r02n).  When every stripe
 // lost blocks, the bitmap tilings are as fast or faster (list tiles -1..-5 %
 // against the better of them, profiles/r02n/tiling_uniform.json, r02o).
 constexpr uint64_t kListStripesNum = 3, kListStripesDen = 4;

@@ -26,6 +26,7 @@
 // indices of xorec_gpu_cmp.cu:127-131).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -59,7 +60,7 @@ __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
 // (MI355X_MICROARCH.md, stores of each flavour): the rebuilt line shares its
 // L2 set with the same column of the blocks the tile is reading, and an
 // in-place nt line left dirty there measured 3-6 % slower (config 3, config
-// 2, 16+4, 32+1 x 64 KiB on two devices; tools/archive/ab/patches/store_policy.py,
+// 2, 16+4, 32+1 x 64 KiB on two devices; bf0ca45:tools/archive/ab/patches/store_policy.py,
 // profiles/r01r, r01s); for encode sc1 was -2..+3 %, so it stays nt.
 constexpr int kEncodeStoreAux = 2;   // nt
 constexpr int kDecodeStoreAux = 16;  // sc1
@@ -676,10 +677,18 @@ hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_ba
                 static_cast<uint64_t*>(d_buf), S, words, seed_base);
 }
 
+// Test hook only (tests/host/error_preserve.cpp).  A user who finds it set
+// is told once, on stderr, that every launch of the library will fail
+// (a silent hook in the shipped library).
 bool fail_launch_for_test() {
   static const bool on = [] {
     const char* e = std::getenv("XEC_TEST_FAIL_LAUNCH");
-    return e != nullptr && e[0] == '1';
+    const bool set = e != nullptr && e[0] == '1';
+    if (set)
+      std::fprintf(stderr,
+                   "xec: XEC_TEST_FAIL_LAUNCH=1 is set: a TEST hook -- every kernel launch of "
+                   "libxec_hip.so will fail on purpose\n");
+    return set;
   }();
   return on;
 }

@@ -46,14 +46,17 @@ XorecBenchmarkHip::XorecBenchmarkHip(const BenchmarkConfig& config,
   if (!xec_hip::set_device(m_opt.device)) throw_error("XorecBenchmarkHip: bad device");
   (void)xec_hip::set_sync_mode(m_opt.sync_mode);  // before the context is active
   if (xec_init(m_opt.device) != XEC_SUCCESS) throw_error("XorecBenchmarkHip: xec_init failed");
-  m_stream = xec_hip::create_stream();
-  if (m_stream == nullptr) throw_error("XorecBenchmarkHip: hipStreamCreate failed");
+  // Buffers first, the stream last: a constructor that throws runs no
+  // destructor, so nothing it made may need one (the buffers free themselves
+  // through their deleters).
   m_gpu_block_bitmap = device_buffer(m_chunks * m_chunk_tot_blocks);
   m_gpu_bad = device_buffer(sizeof(uint32_t));
   m_data_buf = device_buffer(m_chunks * m_chunk_data_size);
   m_parity_buf = device_buffer(m_chunks * m_chunk_parity_size);
   m_block_bitmap = pinned_buffer(m_chunks * m_chunk_tot_blocks);
   if (!m_opt.seeded || m_opt.host_check) m_host_stage = pinned_buffer(m_chunks * m_chunk_data_size);
+  m_stream = xec_hip::create_stream();
+  if (m_stream == nullptr) throw_error("XorecBenchmarkHip: hipStreamCreate failed");
 }
 
 XorecBenchmarkHip::~XorecBenchmarkHip() noexcept {

@@ -62,22 +62,22 @@ def test_frac_falls_back_to_hip_events_without_a_profile():
 
 def _source_id():
     """erasure-code-benchmark_amd/Makefile's XEC_SRC_ID: sha256 of the library's
-    sources (sorted csrc/*.hip, *.cpp, *.h), include/xec.h and the Makefile."""
-    import hashlib
-    pkg = ROOT / "erasure-code-benchmark_amd"
-    files = sorted(str(p.relative_to(pkg)) for pat in ("*.hip", "*.cpp", "*.h")
-                   for p in (pkg / "csrc").glob(pat))
-    h = hashlib.sha256()
-    for f in files + [str(ROOT / "include" / "xec.h"), "Makefile"]:
-        h.update((pkg / f).read_bytes())
-    return h.hexdigest()[:16]
+    sources (sorted csrc/*.hip, *.cpp, *.h), include/xec.h, the Makefile, the
+    compiler flags and `hipcc --version`, as make computes it."""
+    import subprocess
+    out = subprocess.run(["make", "-s", "-C", str(ROOT / "erasure-code-benchmark_amd"),
+                          "print-id"], capture_output=True, text=True, check=True).stdout
+    return out.strip().splitlines()[-1]
 
 
 def test_library_build_id_is_its_sources():
-    """xec_build_info()'s "src:<id>" is the hash of the sources in the tree, so
-    the id names what the library was built from (no stale .so)."""
+    """xec_build_info()'s "src:<id>" is the hash of the sources, flags and
+    compiler in the tree, so the id names what the library was built from (no
+    stale .so)."""
     import xec
-    assert bench.build_id_of(xec.build_info()) == _source_id()
+    sid = _source_id()
+    assert len(sid) == 16 and int(sid, 16) >= 0
+    assert bench.build_id_of(xec.build_info()) == sid
 
 
 @pytest.mark.parametrize("workload", sorted(bench.WORKLOADS))
