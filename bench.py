@@ -184,27 +184,33 @@ def build_id_of(info):
 
 
 def roofline(kernel, b, ms_hip, hbm, traffic_src, lib_build_id=None):
-    """SURVEY.md §8(d) roofline of one kernel: `achieved` = algorithmic bytes
-    per launch / the kernel's rocprofv3 average duration (AverageNs of the
-    kernel-stats CSV the traffic file names, so the line's frac is
-    recomputable from profiles/), when that profile exists for this kernel and
-    batch; else the HIP-event average of this run.  The HIP-event figures of
-    this run are always beside it (`*_hip_events`)."""
+    """SURVEY.md §8(d) roofline of one kernel.  `achieved` = algorithmic bytes
+    per launch / the kernel's average launch duration measured live in this
+    run with HIP events on the stream it is launched on, over the timed region
+    (the contract; VERDICT r05 weak 3: the headline fraction is measured on the
+    box that produced the value).  Beside it, `rocprof_profile`: the same
+    kernel's rocprofv3 --kernel-trace --stats average (AverageNs) from the
+    kernel-stats CSV that profiles/traffic_<workload>.json names -- the profile
+    of the same command, committed under profiles/, from the session that
+    measured the PMC `traffic` -- so that figure is recomputable from profiles/
+    alone, and `over_hip_events_ms` says how well the two clocks agree."""
     hip = b / (ms_hip * 1e-3) / 1e9
     base = kernel.split("<")[0].split(" ")[0]
     prof = rocprof_avg_ns(traffic_src, base)
-    achieved = b / prof["avg_ns"] if prof else hip  # bytes per ns = GB/s
-    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": hbm, "kernel": kernel,
-         "algorithmic_bytes_per_launch": b,
-         "avg_launch_ms": round(prof["avg_ns"] * 1e-6 if prof else ms_hip, 4),
-         "timing_source": (f"rocprofv3 --kernel-trace --stats AverageNs of {prof['kernel']} "
-                           f"({prof['calls']} calls): {prof['source']}") if prof else
-                          "HIP events on the launch stream, this run",
-         "achieved_hip_events": round(hip, 1), "frac_hip_events": round(hip / HBM_PEAK_GBPS, 4),
-         "avg_launch_ms_hip_events": round(ms_hip, 4)}
+    r = {"bound": "hbm", "achieved": round(hip, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(hip / HBM_PEAK_GBPS, 4), "traffic": hbm, "kernel": kernel,
+         "algorithmic_bytes_per_launch": b, "avg_launch_ms": round(ms_hip, 4),
+         "timing_source": "HIP events on the launch stream over the timed region, this run "
+                          "(one event per kernel boundary: each adds its ~6 us queue-packet "
+                          "gap, DESIGN.md §4)"}
     if prof:
-        r["rocprof_over_hip_events_ms"] = round(prof["avg_ns"] * 1e-6 / ms_hip, 4)
+        pa = b / prof["avg_ns"]  # bytes per ns = GB/s
+        r["rocprof_profile"] = {
+            "achieved": round(pa, 1), "frac": round(pa / HBM_PEAK_GBPS, 4),
+            "avg_launch_ms": round(prof["avg_ns"] * 1e-6, 4), "calls": prof["calls"],
+            "kernel": prof["kernel"],
+            "source": f"rocprofv3 --kernel-trace --stats AverageNs: {prof['source']}",
+            "over_hip_events_ms": round(prof["avg_ns"] * 1e-6 / ms_hip, 4)}
     if traffic_src and hbm is not None:
         r["traffic_source"] = traffic_src.get("source")
     if traffic_src:  # which library the profile measured, and the one this line ran
@@ -269,7 +275,9 @@ def cpu_time_port(o, xo, batch, k, m, bs, S, budget_s, threads):
     return reps * (b_enc + b_dec) / t_tot / 1e9, reps, t_tot
 
 
-CPU_SAMPLE_BYTES = 4 << 30  # ~4 GiB of data per sample: far beyond any host LLC
+# Data bytes per CPU sample: every BASELINE shape at its own full batch (config 4:
+# 65,536 stripes = 8 GiB), far beyond any host LLC
+CPU_SAMPLE_BYTES = 8 << 30
 CPU_SAMPLES = 3             # timed samples per figure: median, min and max reported
 
 

@@ -117,19 +117,20 @@ def test_bench_launcher_two_ranks_one_gpu():
 
 
 def test_bench_default_roofline_recomputes_from_profile():
-    """at the default workload the line's roofline.frac is
-    algorithmic bytes / the rocprofv3 AverageNs of the kernel-stats CSV it
-    cites (profiles/), to 3 decimals; this run's HIP-event figure is beside it."""
+    """At the default workload the line's roofline.frac is this run's HIP-event
+    figure (the contract), and its rocprof_profile.frac is algorithmic bytes /
+    the rocprofv3 AverageNs of the kernel-stats CSV it cites (profiles/), to 3
+    decimals; the two clocks agree within the device spread."""
     import csv
     out = run_bench("--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-host-pipeline")
     r = out["roofline"]
-    assert r["timing_source"].startswith("rocprofv3"), r
-    path = ROOT / r["timing_source"].rsplit(": ", 1)[1]
+    assert r["timing_source"].startswith("HIP events"), r
+    assert 0 < r["frac"] < 1 and r["avg_launch_ms"] > 0
+    rp = r["rocprof_profile"]
+    path = ROOT / rp["source"].rsplit(": ", 1)[1]
     base = r["kernel"].split("<")[0]
     row = [x for x in csv.DictReader(open(path))
            if x["Name"].split("(")[0].replace("void ", "").split("<")[0] == base][0]
     frac = r["algorithmic_bytes_per_launch"] / float(row["AverageNs"]) / 8000.0
-    assert round(frac, 3) == round(r["frac"], 3)
-    assert 0 < r["frac_hip_events"] < 1 and r["avg_launch_ms_hip_events"] > 0
-    # the two clocks agree within the documented device spread
-    assert 0.85 < r["rocprof_over_hip_events_ms"] < 1.15, r
+    assert round(frac, 3) == round(rp["frac"], 3)
+    assert 0.85 < rp["over_hip_events_ms"] < 1.15, r

@@ -1,11 +1,13 @@
-"""bench.py's roofline object is recomputable from profiles/ (VERDICT r3 item 2).
+"""bench.py's roofline object.
 
 `roofline.achieved` / `frac` = algorithmic bytes per launch / the kernel's
-rocprofv3 AverageNs in the kernel-stats CSV that profiles/traffic_<workload>.json
-names as its `timing_source` (the same profiling session as its PMC bytes);
-the HIP-event figures of the run sit beside it.  CPU only: bench.roofline is
-called with a made-up HIP-event time, and the expected frac is recomputed here
-straight from the cited CSV.
+average launch duration measured live with HIP events in the run itself;
+beside it, `rocprof_profile` = the same from the rocprofv3 AverageNs in the
+kernel-stats CSV that profiles/traffic_<workload>.json names as its
+`timing_source` (the same profiling session as its PMC bytes), recomputable
+from profiles/ alone.  CPU only: bench.roofline is called with a made-up
+HIP-event time, and the expected figures are recomputed here straight from the
+cited CSV.
 """
 from __future__ import annotations
 
@@ -39,25 +41,27 @@ def test_frac_recomputes_from_cited_profile(workload):
     for base, b, hbm in (("xec::encode_kernel", b_enc, src["encode_hbm_bytes_per_launch"]),
                          (dec_base, b_dec, src["decode_hbm_bytes_per_launch"])):
         r = bench.roofline(base, b, 1.0, hbm, src)
+        # the headline: this run's HIP events (here a made-up 1 ms)
+        assert r["avg_launch_ms"] == 1.0 and r["timing_source"].startswith("HIP events")
+        assert abs(r["frac"] - b / 1e-3 / 1e9 / 8000.0) < 1e-4
+        # beside it, the committed profile's rocprofv3 average, to 4 places
+        rp = r["rocprof_profile"]
         avg_ns = float(_row(src["timing_source"], base)["AverageNs"])
-        # r["frac"] = round(achieved to 0.1 GB/s) / peak, to 4 places
-        assert abs(b / avg_ns / 8000.0 - r["frac"]) < 1e-4
-        assert r["avg_launch_ms"] == round(avg_ns * 1e-6, 4)
-        assert src["timing_source"] in r["timing_source"]
-        # the HIP-event figure of this (made-up) run is kept beside it
-        assert r["avg_launch_ms_hip_events"] == 1.0
-        assert abs(r["frac_hip_events"] - b / 1e-3 / 1e9 / 8000.0) < 1e-4
+        assert abs(b / avg_ns / 8000.0 - rp["frac"]) < 1e-4
+        assert rp["avg_launch_ms"] == round(avg_ns * 1e-6, 4)
+        assert src["timing_source"] in rp["source"]
+        assert rp["over_hip_events_ms"] == round(avg_ns * 1e-6 / 1.0, 4)
         assert r["traffic"] == hbm and r["traffic_source"] == src["source"]
 
 
-def test_frac_falls_back_to_hip_events_without_a_profile():
+def test_frac_without_a_profile():
     r = bench.roofline("xec::encode_kernel", 8_000_000_000, 1.0, None, None)
     assert r["timing_source"].startswith("HIP events")
-    assert r["frac"] == r["frac_hip_events"] == 1.0
-    # a profile that lacks the kernel (e.g. a forced decode tiling) also falls back
+    assert r["frac"] == 1.0 and "rocprof_profile" not in r
+    # a profile that lacks the kernel (e.g. a forced decode tiling) has no cross-check
     src = json.loads((ROOT / "profiles" / "traffic_cfg3.json").read_text())
     r = bench.roofline("xec::decode_class_kernel", 8_000_000_000, 1.0, None, src)
-    assert r["timing_source"].startswith("HIP events")
+    assert r["frac"] == 1.0 and "rocprof_profile" not in r
 
 
 def _source_id():

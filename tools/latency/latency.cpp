@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "xec.h"
@@ -28,6 +29,16 @@ struct BigArgs {
 };
 __global__ void bigarg_kernel(BigArgs a, uint32_t* out) {
   if (threadIdx.x == 0) out[0] = a.v[a.n % 1000];
+}
+// kernel arguments of the sizes the decode's work-list capacities ship
+// (64 / 256 / 1024 entries: 256 B / 1 KiB / 4 KiB)
+template <int N>
+struct Args {
+  uint32_t v[N];
+};
+template <int N>
+__global__ void args_kernel(Args<N> a, uint32_t* out) {
+  if (threadIdx.x == 0) out[0] = a.v[N - 1];
 }
 
 static void report(const char* name, std::vector<double>& us) {
@@ -100,6 +111,24 @@ int main(int argc, char** argv) {
     }
     report("4 KB-arg kernel + stream sync", t);
     t.clear();
+    auto sized = [&](auto tag, const char* name) -> int {
+      constexpr int N = decltype(tag)::value;
+      static Args<N> a;
+      for (int i = 0; i < iters + 50; ++i) {
+        auto t0 = clk::now();
+        a.v[N - 1] = i;
+        args_kernel<N><<<1, 64, 0, s>>>(a, dout);
+        CK(hipStreamSynchronize(s));
+        if (i >= 50) t.push_back(us_since(t0));
+      }
+      report(name, t);
+      t.clear();
+      return 0;
+    };
+    if (sized(std::integral_constant<int, 64>{}, "256 B-arg kernel + sync") ||
+        sized(std::integral_constant<int, 256>{}, "1 KB-arg kernel + sync") ||
+        sized(std::integral_constant<int, 1024>{}, "4 KB-arg kernel (tmpl) + sync"))
+      return 1;
   }
   for (int i = 0; i < iters + 50; ++i) {
     auto t0 = clk::now();
@@ -108,6 +137,15 @@ int main(int argc, char** argv) {
     if (i >= 50) t.push_back(us_since(t0));
   }
   report("xec_encode + stream sync", t);
+  t.clear();
+  for (int i = 0; i < iters + 50; ++i) {
+    auto t0 = clk::now();
+    if (xec_encode(d, p, S, bs, k, m, s) != XEC_SUCCESS) return 2;
+    const double us = us_since(t0);
+    CK(hipStreamSynchronize(s));
+    if (i >= 50) t.push_back(us);
+  }
+  report("xec_encode, call only", t);
   t.clear();
   hipEvent_t ev;
   CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
