@@ -83,6 +83,11 @@ def parse():
                          "device: xec_decode_device (bitmap resident, verdict on the device)")
     ap.add_argument("--decode-tiling", type=int, default=0, choices=[0, 1, 2, 3],
                     help="xec_set_decode_tiling (diagnostic; 0 = the library's automatic choice)")
+    ap.add_argument("--kernel-events", default="dispatch", choices=["dispatch", "packets"],
+                    help="per-kernel timing: dispatch = HIP events recorded by each timed "
+                         "kernel's own dispatch (xec_set_kernel_events), nothing queued "
+                         "between kernels; packets = one hipEventRecord between every two "
+                         "kernels (each a queue packet, ~6 us of gap)")
     ap.add_argument("--dist-world1", action="store_true",
                     help="at N=1, still open a one-rank process group (RCCL with nccl) and run "
                          "the collectives and the scatter/gather leg: exercises the N>1 "
@@ -183,7 +188,16 @@ def build_id_of(info):
     return None
 
 
-def roofline(kernel, b, ms_hip, hbm, traffic_src, lib_build_id=None):
+TIMING_SOURCES = {
+    "dispatch": "HIP events recorded by each timed launch's own dispatch (xec_set_kernel_events "
+                "-> hipExtLaunchKernel) on the launch stream, every timed launch of this run",
+    "packets": "HIP events on the launch stream over the timed region, this run (one "
+               "hipEventRecord per kernel boundary: each adds its ~6 us queue-packet gap, "
+               "DESIGN.md §4)",
+}
+
+
+def roofline(kernel, b, ms_hip, hbm, traffic_src, lib_build_id=None, timing="dispatch"):
     """SURVEY.md §8(d) roofline of one kernel.  `achieved` = algorithmic bytes
     per launch / the kernel's average launch duration measured live in this
     run with HIP events on the stream it is launched on, over the timed region
@@ -200,9 +214,7 @@ def roofline(kernel, b, ms_hip, hbm, traffic_src, lib_build_id=None):
     r = {"bound": "hbm", "achieved": round(hip, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
          "frac": round(hip / HBM_PEAK_GBPS, 4), "traffic": hbm, "kernel": kernel,
          "algorithmic_bytes_per_launch": b, "avg_launch_ms": round(ms_hip, 4),
-         "timing_source": "HIP events on the launch stream over the timed region, this run "
-                          "(one event per kernel boundary: each adds its ~6 us queue-packet "
-                          "gap, DESIGN.md §4)"}
+         "timing_source": TIMING_SOURCES[timing]}
     if prof:
         pa = b / prof["avg_ns"]  # bytes per ns = GB/s
         r["rocprof_profile"] = {
@@ -954,30 +966,45 @@ def run_rank(args):
     # verified for real after the timed region.
     cuda.synchronize()
 
-    # Per-kernel timing: ONE event between every two kernels of the timed
-    # steps (2K+1 in all): events[2i] -> [2i+1] brackets step i's encode,
-    # [2i+1] -> [2i+2] its decode, and step i's last event is step i+1's
-    # first.  Each event is a packet the queue processes between the kernels:
-    # three per step cost 0.8 % of the step, one per kernel boundary 0.4 %
-    # (tools/lab/event_cost.py, profiles/r05s), so none is spent twice.
+    # Per-kernel timing, on the stream the kernels are launched on.  Default
+    # ("dispatch"): every timed encode / decode records a start and a stop HIP
+    # event from its own dispatch (xec_set_kernel_events -> hipExtLaunchKernel),
+    # so the timed region queues nothing but the kernels and each interval is
+    # that kernel's execution alone.  "packets": ONE hipEventRecord between
+    # every two kernels (2K+1 in all), each a queue packet of its own with
+    # ~6 us of gap in the kernel trace (tools/lab/event_cost.py,
+    # profiles/r05s): events[2i] -> [2i+1] brackets step i's encode,
+    # [2i+1] -> [2i+2] its decode.
+    dispatch_events = args.kernel_events == "dispatch"
+
     def step(i, ev=None, stream=stream):
         de, pe, _ = sets[i % NSETS]
         di = (i + NSETS - 1) % NSETS  # the set encoded two kernels ago (module doc)
         dd, pd, _ = sets[di]
+        if ev is not None and dispatch_events:
+            xec.set_kernel_events(ev[0], ev[1])
         rc = xec.encode(de, pe, S, bs, k, m, stream)
-        if ev is not None:
+        if ev is not None and not dispatch_events:
             ev[0].record(stream)
+        if ev is not None and dispatch_events:
+            xec.set_kernel_events(ev[2], ev[3])
         if args.decode_api == "device":
             rc |= xec.decode_device(dd, pd, S, bs, k, m, d_bm, d_status[di:], stream)
         else:
             rc |= xec.decode(dd, pd, S, bs, k, m, h_bm, scratch[di], stream)
-        if ev is not None:
+        if ev is not None and not dispatch_events:
             ev[1].record(stream)
         return rc
 
     for i in range(args.warmup):
         assert step(i) == 0
-    events = [cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
+    if dispatch_events:
+        events = [cuda.Event(enable_timing=True) for _ in range(4 * args.steps)]
+        for e in events:  # torch creates an event's HIP handle at its first record
+            e.record(stream)
+        cuda.synchronize()
+    else:
+        events = [cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
 
     if use_dist:
         dist.barrier()
@@ -985,9 +1012,13 @@ def run_rank(args):
     t0 = time.perf_counter()
     rc = 0
     with markers.timed_region("bench:timed"):
-        events[0].record(stream)
-        for i in range(args.steps):
-            rc |= step(args.warmup + i, events[2 * i + 1:2 * i + 3])
+        if dispatch_events:
+            for i in range(args.steps):
+                rc |= step(args.warmup + i, events[4 * i:4 * i + 4])
+        else:
+            events[0].record(stream)
+            for i in range(args.steps):
+                rc |= step(args.warmup + i, events[2 * i + 1:2 * i + 3])
         cuda.synchronize()
     t1 = time.perf_counter()
     if use_dist:
@@ -996,8 +1027,12 @@ def run_rank(args):
     if args.decode_api == "device":
         assert d_status.tolist() == [0] * NSETS, f"device decode verdicts {d_status.tolist()}"
     elapsed = t1 - t0
-    enc_list = [events[2 * i].elapsed_time(events[2 * i + 1]) for i in range(args.steps)]
-    dec_list = [events[2 * i + 1].elapsed_time(events[2 * i + 2]) for i in range(args.steps)]
+    if dispatch_events:
+        enc_list = [events[4 * i].elapsed_time(events[4 * i + 1]) for i in range(args.steps)]
+        dec_list = [events[4 * i + 2].elapsed_time(events[4 * i + 3]) for i in range(args.steps)]
+    else:
+        enc_list = [events[2 * i].elapsed_time(events[2 * i + 1]) for i in range(args.steps)]
+        dec_list = [events[2 * i + 1].elapsed_time(events[2 * i + 2]) for i in range(args.steps)]
     enc_ms = sum(enc_list) / args.steps
     dec_ms = sum(dec_list) / args.steps
 
@@ -1095,8 +1130,10 @@ def run_rank(args):
         # the dominant kernel is the one the step spends longer in (decode at the
         # BASELINE shapes: in-place writes); both are reported
         lib_id = build_id_of(xec.build_info()) if not args.rehearse_cpu else None
-        rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic, traffic_src, lib_id),
-              "decode": roofline(dec_kernel, b_dec, dec_ms, traffic_dec, traffic_src, lib_id)}
+        rl = {"encode": roofline("xec::encode_kernel", b_enc, enc_ms, traffic, traffic_src, lib_id,
+                                 args.kernel_events),
+              "decode": roofline(dec_kernel, b_dec, dec_ms, traffic_dec, traffic_src, lib_id,
+                                 args.kernel_events)}
         dominant = ("decode" if rl["decode"]["avg_launch_ms"] >= rl["encode"]["avg_launch_ms"]
                     else "encode")
         cpu = None
@@ -1129,7 +1166,8 @@ def run_rank(args):
                        "bytes_convention": "algorithmic: enc S(k+m)bs + dec S(k/m+1)bs",
                        "decode_api": "xec_decode_device" if args.decode_api == "device"
                        else "xec_decode",
-                       "decode_tiling": args.decode_tiling or "automatic"},
+                       "decode_tiling": args.decode_tiling or "automatic",
+                       "kernel_timing": args.kernel_events},
             "roofline": dict(rl[dominant], dominant_by="avg launch time (avg_launch_ms)"),
             # north star: the device-resident rate at every N also as a fraction of
             # the HBM roofline of the N GPUs together (value / (N x 8 TB/s))

@@ -615,8 +615,20 @@ xec_status xec_init(int device_id) {
   return XEC_SUCCESS;
 }
 
+// xec_set_kernel_events arms the next codec call of this thread; that call
+// consumes the setting whether or not it launched a kernel (include/xec.h).
+struct KernelEventsScope {
+  ~KernelEventsScope() { xec::t_kernel_events = xec::KernelEvents{}; }
+};
+
+xec_status xec_set_kernel_events(hipEvent_t start, hipEvent_t stop) {
+  xec::t_kernel_events = xec::KernelEvents{start, stop};
+  return XEC_SUCCESS;
+}
+
 xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, size_t k, size_t m,
                       hipStream_t stream) {
+  const KernelEventsScope events_scope;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
@@ -836,6 +848,7 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
 // device error for the caller, not a std::terminate.
 xec_status xec_decode(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k, size_t m,
                       const uint8_t* h_bitmap, uint8_t* d_bitmap, hipStream_t stream) {
+  const KernelEventsScope events_scope;
   try {
     return decode_impl(d_data, d_parity, S, bs, k, m, h_bitmap, d_bitmap, stream);
   } catch (...) {
@@ -928,6 +941,7 @@ static xec_status decode_per_stripe_impl(void* d_data, const void* d_parity, siz
 xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, size_t bs,
                                  size_t k, size_t m, const uint8_t* h_bitmap, uint8_t* d_bitmap,
                                  uint8_t* h_codes, hipStream_t stream) {
+  const KernelEventsScope events_scope;
   try {  // as xec_decode
     return decode_per_stripe_impl(d_data, d_parity, S, bs, k, m, h_bitmap, d_bitmap, h_codes,
                                   stream);
@@ -939,6 +953,7 @@ xec_status xec_decode_per_stripe(void* d_data, const void* d_parity, size_t S, s
 xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_t bs, size_t k,
                              size_t m, const uint8_t* d_bitmap, int32_t* d_status,
                              hipStream_t stream) {
+  const KernelEventsScope events_scope;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;
@@ -971,6 +986,7 @@ size_t xec_decode_device_list_bytes(size_t S, size_t k, size_t m) {
 xec_status xec_decode_device_list(void* d_data, const void* d_parity, size_t S, size_t bs,
                                   size_t k, size_t m, const uint8_t* d_bitmap, void* d_work,
                                   size_t work_bytes, int32_t* d_status, hipStream_t stream) {
+  const KernelEventsScope events_scope;
   if (!g_initialised.load(std::memory_order_acquire)) return XEC_NOT_INITIALIZED;
   xec_status st = xec_check_args(d_data, d_parity, bs, k, m);
   if (st != XEC_SUCCESS) return st;

@@ -2,6 +2,7 @@
 // gfx950 kernels (xec_kernels.hip).  Not part of the public boundary.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -62,6 +63,15 @@ inline uint32_t grid_for(uint64_t work_items, uint32_t max_grid, uint32_t thread
 // caller's with the same code is pending (tests/host/error_preserve.cpp).
 bool fail_launch_for_test();
 
+// xec_set_kernel_events: events the next codec kernel launch of this thread
+// records from its own dispatch (hipExtLaunchKernel), then forgets.  Set by
+// the ABI call, cleared when the codec call that follows returns
+// (KernelEventsScope, xec_api.cpp), consumed by launch_codec below.
+struct KernelEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local KernelEvents t_kernel_events;
+
 template <typename T>
 struct NoDeduce {
   using type = T;
@@ -79,6 +89,22 @@ hipError_t launch(void (*kernel)(P...), dim3 grid, dim3 block, uint32_t lds, hip
   void* argv[] = {static_cast<void*>(&args)...};
   if (fail_launch_for_test()) block = dim3(2048);
   return hipLaunchKernel(reinterpret_cast<const void*>(kernel), grid, block, argv, lds, s);
+}
+
+// The codec kernels (encode and every decode tiling) go through this: as
+// launch(), but with the thread's pending kernel events, if any, recorded by
+// the kernel's dispatch itself and then cleared.
+template <typename... P>
+hipError_t launch_codec(void (*kernel)(P...), dim3 grid, dim3 block, uint32_t lds, hipStream_t s,
+                        typename NoDeduce<P>::type... args) {
+  const KernelEvents ev = t_kernel_events;
+  if (ev.start == nullptr && ev.stop == nullptr)
+    return launch(kernel, grid, block, lds, s, args...);
+  t_kernel_events = KernelEvents{};
+  void* argv[] = {static_cast<void*>(&args)...};
+  if (fail_launch_for_test()) block = dim3(2048);
+  return hipExtLaunchKernel(reinterpret_cast<const void*>(kernel), grid, block, argv, lds, s,
+                            ev.start, ev.stop, 0);
 }
 
 hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,

@@ -490,7 +490,7 @@ namespace {
 template <int NM, int U, bool NT, int T>
 hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t grid,
                            uint32_t lds, hipStream_t s) {
-  return launch(encode_kernel<NM, U, NT, T>, grid, T, lds, s, static_cast<const uint8_t*>(d),
+  return launch_codec(encode_kernel<NM, U, NT, T>, grid, T, lds, s, static_cast<const uint8_t*>(d),
                 static_cast<uint8_t*>(p), g);
 }
 
@@ -517,25 +517,25 @@ hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geom
   const uint8_t* pp = static_cast<const uint8_t*>(p);
   const uint32_t* list = reinterpret_cast<const uint32_t*>(bm);
   if (tiling == kDecodeDevListTiles)
-    return launch(decode_devlist_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
+    return launch_codec(decode_devlist_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
   if (tiling == kDecodeArgListTiles) {
     switch (arg_items_capacity(al.n)) {
       case 64:
-        return launch(decode_arglist_kernel<NM, U, NT, T, 64>, grid, T, lds, s, dd, pp, g,
+        return launch_codec(decode_arglist_kernel<NM, U, NT, T, 64>, grid, T, lds, s, dd, pp, g,
                       arg_items<64>(al.items, al.n));
       case 256:
-        return launch(decode_arglist_kernel<NM, U, NT, T, 256>, grid, T, lds, s, dd, pp, g,
+        return launch_codec(decode_arglist_kernel<NM, U, NT, T, 256>, grid, T, lds, s, dd, pp, g,
                       arg_items<256>(al.items, al.n));
       default:
-        return launch(decode_arglist_kernel<NM, U, NT, T, 1024>, grid, T, lds, s, dd, pp, g,
+        return launch_codec(decode_arglist_kernel<NM, U, NT, T, 1024>, grid, T, lds, s, dd, pp, g,
                       arg_items<1024>(al.items, al.n));
     }
   }
   if (tiling == kDecodeListTiles)
-    return launch(decode_list_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
+    return launch_codec(decode_list_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, list, g);
   if (tiling == kDecodeClassTiles)
-    return launch(decode_class_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, bm, g);
-  return launch(decode_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, bm, g);
+    return launch_codec(decode_class_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, bm, g);
+  return launch_codec(decode_kernel<NM, U, NT, T>, grid, T, lds, s, dd, pp, bm, g);
 }
 
 // Member counts (k/m) compiled fully unrolled: those of the reference's sweep
@@ -680,6 +680,8 @@ hipError_t launch_fill(void* d_buf, uint64_t S, uint64_t words, uint64_t seed_ba
 // Test hook only (tests/host/error_preserve.cpp).  A user who finds it set
 // is told once, on stderr, that every launch of the library will fail
 // (a silent hook in the shipped library).
+thread_local KernelEvents t_kernel_events;
+
 bool fail_launch_for_test() {
   static const bool on = [] {
     const char* e = std::getenv("XEC_TEST_FAIL_LAUNCH");

@@ -926,6 +926,7 @@ xec_status xec_pipeline_create(xec_pipeline** out, size_t chunk_stripes, size_t 
 }
 
 xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_parity, size_t S) {
+  xec::t_kernel_events = xec::KernelEvents{};  // xec_set_kernel_events is not for the pipeline
   try {
     return encode_impl(p, h_data, h_parity, S);
   } catch (...) {
@@ -935,6 +936,7 @@ xec_status xec_pipeline_encode(xec_pipeline* p, const void* h_data, void* h_pari
 
 xec_status xec_pipeline_decode(xec_pipeline* p, void* h_data, const void* h_parity, size_t S,
                                const uint8_t* h_bitmap) {
+  xec::t_kernel_events = xec::KernelEvents{};  // xec_set_kernel_events is not for the pipeline
   try {
     return decode_impl(p, h_data, h_parity, S, h_bitmap);
   } catch (...) {

@@ -158,7 +158,7 @@ __attribute__((target("avx2,bmi,popcnt"))) int scan_rows_avx2(const uint8_t* bm,
              _mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_and_si256(x1, one), zero)))) << 32);
     need |= e & data_mask;
     uint64_t zd = z & data_mask;
-    if (items != nullptr) {  // lost data blocks, in order (rare: most rows have none)
+    if (items != nullptr && lost < cap) {  // lost data blocks, in order, until the list is full
       for (uint64_t q = lost; zd; zd &= zd - 1, ++q)
         if (q < cap) items[q] = xec_work_item(c, static_cast<size_t>(__builtin_ctzll(zd)));
       zd = z & data_mask;

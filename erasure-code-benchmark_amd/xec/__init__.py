@@ -10,7 +10,8 @@ from .codec import (DECODE_KERNELS, Pipeline, build_info, check_args, check_bitm
                     decode_per_stripe, decode_tiling_used,
                     device_list_bytes, encode, erase,
                     fill_splitmix64, init,
-                    select_lost_blocks, set_decode_tiling, set_launch, set_occupancy,
+                    select_lost_blocks, set_decode_tiling, set_kernel_events, set_launch,
+                    set_occupancy,
                     set_rotation, set_validate_kernel,
                     status_string, validate_blocks, write_validation_pattern)
 from .partition import stripe_range
@@ -21,6 +22,7 @@ __all__ = [
     "decode_device", "decode_device_list",
     "decode_per_stripe", "decode_tiling_used", "device_list_bytes",
     "encode", "erase", "fill_splitmix64", "init", "select_lost_blocks", "set_decode_tiling",
+    "set_kernel_events",
     "set_launch",
     "set_occupancy", "set_rotation", "set_validate_kernel", "status_string", "stripe_range", "validate_blocks",
     "write_validation_pattern",

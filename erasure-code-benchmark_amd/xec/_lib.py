@@ -29,7 +29,7 @@ EXPORTED = (
     "xec_set_validate_kernel", "xec_decode_tiling_used", "xec_decode_per_stripe",
     "xec_decode_device_list", "xec_decode_device_list_bytes", "xec_get_tuning",
     "xec_set_tuning", "xec_set_rotation", "xec_select_lost_blocks",
-    "xec_decode_arg_capacity_used", "xec_peer_link",
+    "xec_decode_arg_capacity_used", "xec_peer_link", "xec_set_kernel_events",
 )
 
 
@@ -95,6 +95,7 @@ def lib() -> ctypes.CDLL:
         "xec_decode_tiling_used": ([], ctypes.c_int),
         "xec_decode_arg_capacity_used": ([], ctypes.c_int),
         "xec_peer_link": ([ctypes.c_int, ctypes.c_int, vp], st),
+        "xec_set_kernel_events": ([vp, vp], st),
         "xec_decode_per_stripe": ([vp, vp, sz, sz, sz, sz, vp, vp, vp, vp], st),
         "xec_status_string": ([st], ctypes.c_char_p),
         "xec_build_info": ([], ctypes.c_char_p),

@@ -164,6 +164,22 @@ def decode_tiling_used() -> int:
     return int(lib().xec_decode_tiling_used())
 
 
+def set_kernel_events(start, stop) -> Status:
+    """xec_set_kernel_events: the calling thread's next codec call launches its
+    kernel with these events, recorded by the kernel's own dispatch
+    (hipExtLaunchKernel); `start` / `stop` are torch.cuda.Event objects (or
+    None).  torch creates an event's HIP handle at its first record(), so each
+    must have been recorded once before."""
+    def handle(ev):
+        if ev is None:
+            return None
+        h = int(ev.cuda_event)
+        if not h:
+            raise ValueError("record the torch.cuda.Event once before handing it over")
+        return ctypes.c_void_p(h)
+    return Status(lib().xec_set_kernel_events(handle(start), handle(stop)))
+
+
 def decode_arg_capacity_used() -> int:
     """xec_decode_arg_capacity_used: after a kernel-argument list decode, the
     capacity its arguments carried (64, 256 or 1024 entries); else 0."""

@@ -36,6 +36,7 @@ extern "C" {
 #endif
 
 typedef struct ihipStream_t* hipStream_t;
+typedef struct ihipEvent_t* hipEvent_t;
 
 typedef enum {
   XEC_SUCCESS = 0,           /* XorecResult::Success */
@@ -300,6 +301,20 @@ int xec_decode_tiling_used(void);
  * launch could hold -- 64, 256 or 1024, the smallest capacity that holds the
  * list, so a short list ships short kernel arguments; 0 for any other tiling. */
 int xec_decode_arg_capacity_used(void);
+
+/* Diagnostics / measurement: the calling thread's NEXT xec_encode, xec_decode,
+ * xec_decode_per_stripe, xec_decode_device or xec_decode_device_list call
+ * launches its encode / decode kernel with hipExtLaunchKernel and these two
+ * events (either may be NULL), which the runtime records from that kernel's
+ * own dispatch: hipEventElapsedTime(start, stop) is the kernel's execution
+ * time, with no event packet queued between kernels (a hipEventRecord between
+ * two kernels is a queue packet of its own, ~6 us of gap in the kernel trace,
+ * DESIGN.md §4).  Both must be events of the stream's device created with
+ * timing enabled.  The call that follows consumes the setting whether or not
+ * it launches a kernel (a decode with nothing to rebuild records nothing); a
+ * per-stripe decode that launches in pieces times its first piece.  The
+ * pipeline calls ignore and clear it. */
+xec_status xec_set_kernel_events(hipEvent_t start, hipEvent_t stop);
 
 /* ---- host-in / host-out pipeline --------------------
  * The MI355X analogue of the reference's GPU-memory / unified-memory variants

@@ -50,7 +50,25 @@ class CpuXec:
             v[c] = _splitmix(seed_base + c, stripe_bytes // 8)
         return 0
 
+    _events = None  # xec_set_kernel_events stand-in: (start, stop) for the next call
+
+    def set_kernel_events(self, start, stop):
+        self._events = (start, stop)
+        return 0
+
+    def _timed(self, fn):
+        ev, self._events = self._events, None
+        if ev and ev[0] is not None:
+            ev[0].record()
+        rc = fn()
+        if ev and ev[1] is not None:
+            ev[1].record()
+        return rc
+
     def encode(self, d, p, S, bs, k, m, stream=None):
+        return self._timed(lambda: self._encode(d, p, S, bs, k, m))
+
+    def _encode(self, d, p, S, bs, k, m):
         if S == 0:
             return 0
         blocks = _np(d)[: S * k * bs].reshape(S, k // m, m, bs)
@@ -69,11 +87,11 @@ class CpuXec:
         return 0
 
     def decode(self, d, p, S, bs, k, m, h_bm, d_bm=None, stream=None):
-        return self._rebuild(d, p, S, bs, k, m, _np(h_bm))
+        return self._timed(lambda: self._rebuild(d, p, S, bs, k, m, _np(h_bm)))
 
     def decode_device(self, d, p, S, bs, k, m, d_bm, d_status, stream=None):
         _np(d_status)[0] = 0
-        return self._rebuild(d, p, S, bs, k, m, _np(d_bm))
+        return self._timed(lambda: self._rebuild(d, p, S, bs, k, m, _np(d_bm)))
 
     def erase(self, d, p, S, bs, k, m, d_bm, stream=None):
         data = _np(d)[: S * k * bs].reshape(S, k, bs)
