@@ -64,6 +64,12 @@ int main(int argc, char** argv) {
   const size_t bs = argc > 4 ? std::strtoull(argv[4], nullptr, 10) : 1024;
   const size_t S = argc > 5 ? std::strtoull(argv[5], nullptr, 10) : (8u << 20) / (k * 1024);
   const int iters = argc > 6 ? std::atoi(argv[6]) : 2000;
+  // lost data blocks per stripe, one per parity class (classes 0 .. lost-1)
+  const size_t lost = argc > 7 ? std::strtoull(argv[7], nullptr, 10) : 1;
+  if (lost < 1 || lost > m) {
+    std::fprintf(stderr, "lost per stripe must be 1..m\n");
+    return 2;
+  }
   static const unsigned flags[] = {hipDeviceScheduleAuto, hipDeviceScheduleSpin,
                                    hipDeviceScheduleYield, hipDeviceScheduleBlockingSync};
   CK(hipSetDeviceFlags(flags[mode & 3]));
@@ -187,13 +193,21 @@ int main(int argc, char** argv) {
   }
   report("encode device time (events)", t);
   t.clear();
-  // decode: one lost data block per stripe, (7c) mod k (bench.py's pattern)
+  // decode: `lost` data blocks per stripe; with one, (7c) mod k (bench.py's
+  // pattern), with more, block j + m * ((7c) mod (k/m)) of classes j < lost
   uint8_t* h_bm;
   uint8_t* d_bm;
   CK(hipHostMalloc(reinterpret_cast<void**>(&h_bm), S * (k + m), hipHostMallocDefault));
   CK(hipMalloc(reinterpret_cast<void**>(&d_bm), S * (k + m)));
-  for (size_t c = 0; c < S; ++c)
-    for (size_t i = 0; i < k + m; ++i) h_bm[c * (k + m) + i] = i == (7 * c) % k ? 0 : 1;
+  for (size_t c = 0; c < S; ++c) {
+    for (size_t i = 0; i < k + m; ++i) h_bm[c * (k + m) + i] = 1;
+    if (lost == 1) {
+      h_bm[c * (k + m) + (7 * c) % k] = 0;
+    } else {
+      for (size_t j = 0; j < lost; ++j) h_bm[c * (k + m) + j + m * ((7 * c) % (k / m))] = 0;
+    }
+  }
+  std::printf("decode: %zu lost data block(s) per stripe, %zu in all\n", lost, lost * S);
   for (int tiling : {0, 3}) {
     if (xec_set_decode_tiling(tiling) != XEC_SUCCESS) return 2;
     for (int i = 0; i < iters + 50; ++i) {
