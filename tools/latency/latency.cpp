@@ -10,6 +10,7 @@
 // block per stripe, pinned host bitmap) + stream sync with the automatic and
 // the work-list tiling; and xec_decode of a batch without losses, alone and
 // + stream sync.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,6 +40,14 @@ struct Args {
 template <int N>
 __global__ void args_kernel(Args<N> a, uint32_t* out) {
   if (threadIdx.x == 0) out[0] = a.v[N - 1];
+}
+
+// xec_set_kernel_events is new in round 6: looked up at run time, so this
+// tool still runs against an older libxec_hip.so (LD_LIBRARY_PATH) and then
+// skips the dispatch-timed measurements
+using SetEvents = xec_status (*)(hipEvent_t, hipEvent_t);
+static SetEvents set_events() {
+  return reinterpret_cast<SetEvents>(dlsym(RTLD_DEFAULT, "xec_set_kernel_events"));
 }
 
 static void report(const char* name, std::vector<double>& us) {
@@ -74,6 +83,10 @@ int main(int argc, char** argv) {
                                    hipDeviceScheduleYield, hipDeviceScheduleBlockingSync};
   CK(hipSetDeviceFlags(flags[mode & 3]));
   if (xec_init(0) != XEC_SUCCESS) return 1;
+  // XEC_LAT_OCC=n: xec_set_occupancy(n) for every codec call of this run
+  // (0 automatic, 1..7 waves per SIMD, 8 no cap)
+  if (const char* o = std::getenv("XEC_LAT_OCC"); o != nullptr && *o != '\0')
+    if (xec_set_occupancy(std::atoi(o)) != XEC_SUCCESS) return 1;
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   void *d, *p;
@@ -193,6 +206,18 @@ int main(int argc, char** argv) {
   }
   report("encode device time (events)", t);
   t.clear();
+  // the encode kernel alone: events recorded by its own dispatch
+  const SetEvents arm = set_events();
+  for (int i = 0; arm != nullptr && i < 500; ++i) {
+    if (arm(e0, e1) != XEC_SUCCESS) return 2;
+    if (xec_encode(d, p, S, bs, k, m, s) != XEC_SUCCESS) return 2;
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    t.push_back(ms * 1e3);
+  }
+  if (arm != nullptr) report("encode kernel (dispatch)", t);
+  t.clear();
   // decode: `lost` data blocks per stripe; with one, (7c) mod k (bench.py's
   // pattern), with more, block j + m * ((7c) mod (k/m)) of classes j < lost
   uint8_t* h_bm;
@@ -220,6 +245,16 @@ int main(int argc, char** argv) {
     t.clear();
   }
   xec_set_decode_tiling(0);
+  for (int i = 0; arm != nullptr && i < 500; ++i) {
+    if (arm(e0, e1) != XEC_SUCCESS) return 2;
+    if (xec_decode(d, p, S, bs, k, m, h_bm, d_bm, s) != XEC_SUCCESS) return 2;
+    CK(hipStreamSynchronize(s));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    t.push_back(ms * 1e3);
+  }
+  if (arm != nullptr) report("decode kernel (dispatch)", t);
+  t.clear();
   // the host time of the decode call alone (its stream synchronised outside
   // the timed region): what a caller that does not wait pays per call
   for (int i = 0; i < iters + 50; ++i) {
