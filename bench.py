@@ -1210,7 +1210,7 @@ def run_rank(args):
                     if args.steps >= NSETS else None for q in range(NSETS)]
                 for n, v, shift in (("encode", enc_list, 0), ("decode", dec_list, NSETS - 1))},
         }
-        if world > 1:
+        if use_dist:
             # how the scatter leg's bytes travel from rank 0's GPU to each rank's
             # (a CPU rehearsal stands for an N-GPU node: rank r on device r)
             out["topology"] = scatter_topology(

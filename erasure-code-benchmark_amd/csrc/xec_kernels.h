@@ -128,8 +128,9 @@ constexpr uint32_t kDevListHeader = 1;  // u32 words before the first entry
 // The list travels in the kernel arguments, so a launch ships the whole array
 // whatever the list's length: each kernel that takes one is compiled for three
 // capacities and the launch picks the smallest that holds the list (VERDICT
-// r05 item 4: 4 KiB of arguments cost 1.5-2.1 us per synchronous call against
-// an empty kernel, profiles/r03zn).
+// r05 item 4).  A kernel with 4 KiB of arguments costs 0.15-0.4 us more per
+// synchronous call than the same kernel with 256 B (tools/latency,
+// profiles/r06b): small, but free to avoid.
 constexpr uint64_t kArgItems = 1024;  // the largest capacity
 template <uint32_t N>
 struct ArgItems {

@@ -490,8 +490,8 @@ namespace {
 template <int NM, int U, bool NT, int T>
 hipError_t launch_encode_t(const void* d, void* p, const Geometry& g, uint32_t grid,
                            uint32_t lds, hipStream_t s) {
-  return launch_codec(encode_kernel<NM, U, NT, T>, grid, T, lds, s, static_cast<const uint8_t*>(d),
-                static_cast<uint8_t*>(p), g);
+  return launch_codec(encode_kernel<NM, U, NT, T>, grid, T, lds, s,
+                      static_cast<const uint8_t*>(d), static_cast<uint8_t*>(p), g);
 }
 
 // The first n of h_items in an ArgItems<CAP>, the rest zero (the kernel never

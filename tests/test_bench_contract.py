@@ -101,6 +101,8 @@ def test_bench_rccl_world1():
     sc = out["scatter"]
     assert sc.get("bit_exact") is True, sc
     assert sc["gathered_parity_bit_exact_vs_root_encode"] is True
+    # the topology record at world 1: the root reaches only itself
+    assert out["topology"]["path"] == "local" and sc["path"] == "local", out["topology"]
     assert out["host_pipeline"]["bit_exact"] is True
 
 
