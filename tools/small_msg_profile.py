@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--lines", default="", help="comma list of reference lines (default: all 24)")
+    ap.add_argument("--no-prof", action="store_true", help="call times only, no rocprofv3 runs")
     args = ap.parse_args()
     env = dict(os.environ)
     if args.lib:
@@ -100,13 +102,17 @@ def main():
     out_path = Path(args.out)
     out_path.parent.mkdir(parents=True, exist_ok=True)
     cfgs = reference_rows()
+    if args.lines:
+        keep = {int(x) for x in args.lines.split(",")}
+        cfgs = [c for c in cfgs if c["ref_line"] in keep]
     plain = run_bench(cfgs, args.iters, args.warmup, env)
     assert len(plain) == len(cfgs), (len(plain), len(cfgs))
     rows = []
     for c, o in zip(cfgs, plain):
         pdir = out_path.parent / f"prof_{args.tag or 'wt'}_{c['ref_line']}"
-        run_bench([c], args.iters, args.warmup, env, prof_dir=pdir)
-        st = kernel_stats(pdir)
+        if not args.no_prof:
+            run_bench([c], args.iters, args.warmup, env, prof_dir=pdir)
+        st = {} if args.no_prof else kernel_stats(pdir)
         en, ev = pick(st, "encode_kernel")
         dn, dv = pick(st, "decode_")
         S = MESSAGE // (c["k"] * c["block_B"])
