@@ -1,9 +1,10 @@
 """RCCL point-to-point on the GPU box (one GPU): the batched send / recv that
 xec/dist.py's scatter and gather post (batch_isend_irecv on both ends) run
-over RCCL here as a send to self inside one batch, bit-exact, plus the
-world-1 scatter / gather (the root's own slice).  The N > 1 transfers between
-GPUs are the driver's 8-GPU runs; tests/test_distributed_cpu.py covers their
-bookkeeping under gloo."""
+over RCCL here as a send to self inside one batch, bit-exact -- messages past
+2^32 bytes, and config 5's whole root-side group at N = 8 (7 peers x 16
+pieces of 256 MiB, 112 sends) -- plus the world-1 scatter / gather (the root's
+own slice).  Between distinct GPUs, tests/test_gpu_multi_rank.py (two or more
+GPUs); tests/test_distributed_cpu.py covers the bookkeeping under gloo."""
 from __future__ import annotations
 
 import subprocess
