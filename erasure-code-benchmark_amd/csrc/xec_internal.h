@@ -23,14 +23,19 @@ struct XecScan {
   uint64_t stripes_lost = 0;  // stripes with at least one zero data byte
   int64_t lost_class = -1;    // the parity class every lost data block is in, or -1
                               // (none lost, or several classes): one failed device
+  uint64_t listed = 0;        // work items written; the list is whole iff == lost_data
 };
 
 // xec_check_bitmap plus the counts above (out may be null) and, when `items`
 // is non-null, the first `cap` lost data blocks as work items in batch order
-// (requires k <= kWorkItemMaxK and S <= kWorkItemMaxStripes).  Defined in
-// xec_scan.cpp.
+// (requires k <= kWorkItemMaxK and S <= kWorkItemMaxStripes).  `speculative`:
+// the caller may not need the list at all, so listing stops once the losses
+// seen so far, projected over the batch, say it will not be used -- more than
+// `cap` of them, or a batch dense enough for class tiles (lost > S and
+// 2 * lost >= S * m, xec_api.cpp use_class_tiles) -- and out->listed tells how
+// many were written.  Defined in xec_scan.cpp.
 xec_status xec_scan_bitmap(const uint8_t* h_bitmap, size_t S, size_t k, size_t m, XecScan* out,
-                           uint32_t* items, uint64_t cap);
+                           uint32_t* items, uint64_t cap, bool speculative = false);
 
 // Per-stripe form (the reference CPU plugin's loop, xorec_bm.cpp:43-58 over
 // xorec_decode, xorec.cpp:62-111): codes[c] (if non-null) = 0 or 4

@@ -8,6 +8,7 @@
 // against a direct enumeration.
 //   g++ -std=c++17 -O1 -g -fsanitize=address,undefined -I include \
 //       tests/host/scan_fuzz.cpp erasure-code-benchmark_amd/csrc/xec_scan.cpp
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <random>
@@ -34,11 +35,11 @@ static int reference(const uint8_t* bm, size_t S, size_t k, size_t m, int* need)
 int main() {
   std::mt19937_64 rng(1896);
   const size_t ms[] = {1, 2, 3, 4, 5, 8, 16, 32};
-  long cases = 0;
+  long cases = 0, spec_stops = 0;
   for (int trial = 0; trial < 20000; ++trial) {
     const size_t m = ms[rng() % 8];
     const size_t k = m * (1 + rng() % (trial % 3 == 0 ? 80 : 12));
-    const size_t S = rng() % 40;
+    const size_t S = rng() % (trial % 11 == 0 ? 400 : 40);  // some past the 32-row projection
     const double p_loss = (rng() % 4) * 0.04;
     const size_t n = S * (k + m);
     uint8_t* bm = new uint8_t[n ? n : 1];
@@ -71,8 +72,19 @@ int main() {
     }
     const bool stripes_ok = got2 != XEC_SUCCESS || scan.stripes_lost == stripes_ref;
     bool items_ok = true;
-    if (items != nullptr && got2 == XEC_SUCCESS)
+    if (items != nullptr && got2 == XEC_SUCCESS) {
       for (uint64_t q = 0; q < cap; ++q) items_ok &= items[q] == items_ref[q];
+      items_ok &= scan.listed == cap;
+      // speculative listing (decode's first pass): may stop early, never lies --
+      // the `listed` items it reports are the reference's first ones
+      XecScan sp;
+      std::fill(items, items + (cap ? cap : 1), 0xFFFFFFFFu);
+      const xec_status got3 = xec_scan_bitmap(bm, S, k, m, &sp, items, cap, true);
+      items_ok &= got3 == got2 && sp.lost_data == scan.lost_data && sp.listed <= cap;
+      for (uint64_t q = 0; items_ok && q < sp.listed; ++q) items_ok &= items[q] == items_ref[q];
+      // (how often the projection stopped a list early)
+      if (items_ok && sp.listed < cap) ++spec_stops;
+    }
     delete[] items;
     std::vector<uint8_t> bm_keep(bm, bm + n);
     delete[] bm;
@@ -118,6 +130,7 @@ int main() {
   int need = 0;
   if (xec_check_bitmap(nullptr, 0, 4, 1, &need) != XEC_SUCCESS || need != 0) return 1;
   if (xec_check_bitmap(nullptr, 0, 3, 2, &need) != XEC_INVALID_COUNTS) return 1;
-  std::printf("scan_fuzz ok: %ld cases\n", cases);
+  std::printf("scan_fuzz ok: %ld cases (%ld speculative lists stopped early)\n", cases,
+              spec_stops);
   return 0;
 }
