@@ -35,7 +35,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default="")
+    ap.add_argument("--grids", default="",
+                    help="comma list of extra xec_set_launch max_grid values for the list "
+                         "decode (variants list_g<N>)")
     args = ap.parse_args()
+    grids = [int(x) for x in args.grids.split(",") if x]
     import numpy as np
     import torch
 
@@ -60,10 +64,14 @@ def main():
             d_bm = torch.from_numpy(bm.reshape(-1)).to("cuda")
             lost = len(rows)
 
+            variants = ["device", "list", "list_full"] + [f"list_g{g}" for g in grids]
+
             def run(variant):
                 if variant == "device":
                     return xec.decode_device(d, p, S, bs, k, m, d_bm, status, s)
-                assert xec.set_launch(0, (1 << 31) - 1 if variant == "list_full" else 0, 0, 0) == 0
+                mg = ((1 << 31) - 1 if variant == "list_full" else
+                      int(variant[6:]) if variant.startswith("list_g") else 0)
+                assert xec.set_launch(0, mg, 0, 0) == 0
                 try:
                     return xec.decode_device_list(d, p, S, bs, k, m, d_bm, work, work.numel(),
                                                   status, s)
@@ -71,7 +79,7 @@ def main():
                     xec.set_launch(0, 0, 0, 0)
 
             ref = None
-            for v in ("device", "list", "list_full"):  # the same bytes from every variant
+            for v in variants:  # the same bytes from every variant
                 assert xec.erase(d, p, S, bs, k, m, d_bm, s) == 0
                 assert run(v) == 0
                 torch.cuda.synchronize()
@@ -80,7 +88,7 @@ def main():
                 ref = got if ref is None else ref
                 assert torch.equal(got, ref), (name, density, v)
             del ref, got
-            times = {v: [] for v in ("device", "list", "list_full")}
+            times = {v: [] for v in variants}
             for _ in range(args.rounds):
                 for v in times:
                     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
