@@ -575,6 +575,8 @@ xec::LaunchShape launch_shape(size_t bs, int auto_w) {
 // workgroups per CU its LDS reservation admits, at most 32 waves per CU):
 // the fixed grid of decode_devlist_kernel, which walks a count the host never
 // sees.  0 if the device cannot be queried.
+constexpr uint64_t kDevListMaxGrid = 131072;  // xec_decode_device_list's largest default grid
+
 uint32_t resident_workgroups(const xec::LaunchShape& ls) {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -1003,15 +1005,27 @@ xec_status xec_decode_device_list(void* d_data, const void* d_parity, size_t S, 
   if (S == 0)
     return hipMemsetAsync(d_status, 0, sizeof(int32_t), stream) == hipSuccess ? XEC_SUCCESS
                                                                               : XEC_DEVICE_ERROR;
-  // one reduction per tile, as encode: encode's residency table; the grid is
-  // what the chip holds at once (on the stream's device) unless xec_set_launch
-  // gave max_grid
+  // One reduction per tile, as encode: encode's residency table.  The list's
+  // length is known only on the device, so the decode walks it with a grid
+  // fixed at launch (unless xec_set_launch gave max_grid): one workgroup per
+  // 8 possible tiles (S*m entries x chunks), at least what the chip holds at
+  // once (on the stream's device) and at most kDevListMaxGrid.  A grid past
+  // the list's end costs ~0.17 ns per idle workgroup; a grid of only what the
+  // chip holds walks a dense list 5-18 % slower than one workgroup per tile.
+  // Against that resident-only grid this was 3-5 % faster on dense lists and
+  // 1-8 % on sparse ones (configs 2-4, 16+8 x 64 KiB, every stripe or 1 in 9
+  // losing a block; tools/lab/devlist_grid.py, profiles/r06n).
   const StreamDevice sd(stream);
   if (!sd.ok()) return XEC_DEVICE_ERROR;
   xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
-  if (ls.max_grid == 0) ls.max_grid = resident_workgroups(ls);
-  if (ls.max_grid == 0) return XEC_DEVICE_ERROR;
   xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+  if (ls.max_grid == 0) {
+    const uint64_t resident = resident_workgroups(ls);
+    if (resident == 0) return XEC_DEVICE_ERROR;
+    const uint64_t eighth = (uint64_t)S * m * g.tiles_per_block / 8;
+    const uint64_t want = eighth < kDevListMaxGrid ? eighth : kDevListMaxGrid;
+    ls.max_grid = (uint32_t)(want > resident ? want : resident);
+  }
   uint32_t* list = static_cast<uint32_t*>(d_work);
   if (xec::launch_scan_list(d_bitmap, g, d_status, list, stream) != hipSuccess)
     return XEC_DEVICE_ERROR;

@@ -340,13 +340,15 @@ __global__ __launch_bounds__(T) void decode_arglist_kernel(uint8_t* data,
 
 // The same with a list the device built (xec_decode_device_list): list[0] is
 // the entry count scan_list_kernel left, entries from list[1].  The host
-// never sees the count, so the launch is a fixed grid of about what the chip
-// holds at once, walking the count's tiles in grid strides.  On sparse
-// batches that is 1.8-3.7x faster than decode_kernel over every stripe; on
-// dense ones 5-19 % slower than one workgroup per tile, and handing the tiles
-// out in order from per-XCD work-queue heads instead was no better (0-31 %
-// behind, commit 6f8fb1e, profiles/r02af, r02ag, r02ah), so the walk stays
-// simple.  The gate is the check's verdict, as in decode_kernel.
+// never sees the count, so the launch is a fixed grid (xec_api.cpp: one
+// workgroup per 8 possible tiles, between what the chip holds at once and
+// 131,072), walking the count's tiles in grid strides; workgroups past the
+// list's end return at once.  On sparse batches that is 2-4x faster than
+// decode_kernel over every stripe, and on dense ones within 1-4 % of one
+// workgroup per tile (profiles/r06n); handing the tiles out in order from
+// per-XCD work-queue heads instead was no better (0-31 % behind, commit
+// 6f8fb1e, profiles/r02af, r02ag, r02ah), so the walk stays simple.  The gate
+// is the check's verdict, as in decode_kernel.
 template <int NM, int U, bool NT, int T>
 __global__ __launch_bounds__(T) void decode_devlist_kernel(uint8_t* data,
                                                            const uint8_t* __restrict__ parity,
