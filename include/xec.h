@@ -146,11 +146,12 @@ xec_status xec_decode_device(void* d_data, const void* d_parity, size_t S, size_
  * workgroups finding nothing to do.  Here the check kernel also lists the
  * lost data blocks into d_work (4-byte aligned device scratch of at least
  * xec_decode_device_list_bytes(S, k, m) bytes, owned by the caller), and the
- * decode is one tile per (listed block, chunk), walked by a fixed grid of
- * about what the chip holds at once (xec_set_launch's max_grid overrides it),
- * since the host never sees the count.  Sparse losses (1 stripe in 9): about
- * 2x faster than xec_decode_device; losses in every stripe: 5-19 % slower,
- * so there xec_decode_device is the better call.  Everything else as xec_decode_device: no
+ * decode is one tile per (listed block, chunk), walked by a grid fixed at
+ * launch since the host never sees the count: one workgroup per 8 possible
+ * tiles, between what the chip holds at once and 131,072 (xec_set_launch's
+ * max_grid overrides it).  Sparse losses (1 stripe in 9): 1.7-3.9x faster
+ * than xec_decode_device; losses in every stripe: 6-13 % slower, so there
+ * xec_decode_device is the better call.  Everything else as xec_decode_device: no
  * host work (hipGraph-capturable), *d_status = 0 or 4 in stream order,
  * all-or-nothing, parity read-only, identical bytes.  Requires k <= 256 and
  * S <= 2^24 (else XEC_INVALID_SIZE), as does a too small work_bytes or a null
