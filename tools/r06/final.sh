@@ -22,4 +22,6 @@ timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err
 tail -c 300 $O/bench.json
 timeout -k 10 300 python3 bench.py --dist-world1 --no-cpu-baseline --multi-devices 0,0 \
   > $O/bench_world1_multi.json 2> $O/bench_world1_multi.err
+XEC_FUZZ_CASES=2500 XEC_FUZZ_SEED=92000 timeout -k 10 400 python -u -m pytest tests/test_gpu_fuzz.py -x -q --timeout 300 --timeout-method thread > $O/pytest_fuzz.txt 2>&1 || { tail -30 $O/pytest_fuzz.txt; exit 1; }
+tail -1 $O/pytest_fuzz.txt
 echo "final done"
