@@ -11,6 +11,7 @@
 // the work-list tiling; and xec_decode of a batch without losses, alone and
 // + stream sync.
 #include <dlfcn.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,6 +41,25 @@ struct Args {
 template <int N>
 __global__ void args_kernel(Args<N> a, uint32_t* out) {
   if (threadIdx.x == 0) out[0] = a.v[N - 1];
+}
+
+// Latency probes (round 6, DESIGN.md §4 *Small messages*): one-wave
+// workgroups, one 1 KiB chunk each, like the codec's tiles.  load_probe only
+// loads (the store is never taken), store_probe only stores, copy_probe loads
+// then stores: timed from their own dispatch they split a small codec
+// kernel's time into dispatch, load round trip and store drain.
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+__global__ void load_probe(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint32_t key) {
+  const u32x4 v = __builtin_nontemporal_load(src + blockIdx.x * 64 + threadIdx.x);
+  if (v.x == key && v.y == key + 1) dst[blockIdx.x * 64 + threadIdx.x] = v;
+}
+__global__ void store_probe(u32x4* __restrict__ dst, uint32_t key) {
+  const u32x4 v = {key, blockIdx.x, threadIdx.x, 0u};
+  __builtin_nontemporal_store(v, dst + blockIdx.x * 64 + threadIdx.x);
+}
+__global__ void copy_probe(const u32x4* __restrict__ src, u32x4* __restrict__ dst) {
+  const u32x4 v = __builtin_nontemporal_load(src + blockIdx.x * 64 + threadIdx.x);
+  __builtin_nontemporal_store(v, dst + blockIdx.x * 64 + threadIdx.x);
 }
 
 // xec_set_kernel_events is new in round 6: looked up at run time, so this
@@ -109,6 +129,46 @@ int main(int argc, char** argv) {
   }
   report("empty kernel + stream sync", t);
   t.clear();
+  for (int i = 0; i < iters + 50; ++i) {
+    auto t0 = clk::now();
+    empty_kernel<<<1, 64, 0, s>>>();
+    const double us = us_since(t0);
+    CK(hipStreamSynchronize(s));
+    if (i >= 50) t.push_back(us);
+  }
+  report("empty kernel, call only", t);
+  t.clear();
+  // the copy probe over the batch's 1 KiB tiles (the encode's grid at m = 1),
+  // launched with <<<>>>, without and with an LDS reservation of L bytes
+  // (XEC_LAT_LDS, default 10240: the residency cap's reservation at 8 members)
+  {
+    const uint32_t tiles = (uint32_t)std::min<size_t>(S * m * bs / 1024, S * k * bs / 1024);
+    const char* le = std::getenv("XEC_LAT_LDS");
+    const uint32_t lds = le != nullptr && *le != '\0' ? (uint32_t)std::atoi(le) : 10240u;
+    for (uint32_t l : {0u, lds}) {
+      for (int i = 0; i < iters + 50; ++i) {
+        auto t0 = clk::now();
+        hipLaunchKernelGGL(copy_probe, dim3(tiles), dim3(64), l, s,
+                           static_cast<const u32x4*>(d), static_cast<u32x4*>(p));
+        CK(hipStreamSynchronize(s));
+        if (i >= 50) t.push_back(us_since(t0));
+      }
+      char nm[64];
+      std::snprintf(nm, sizeof nm, "copy x%u lds %u + sync", tiles, l);
+      report(nm, t);
+      t.clear();
+    }
+    for (int i = 0; i < iters + 50; ++i) {
+      auto t0 = clk::now();
+      hipLaunchKernelGGL(copy_probe, dim3(tiles), dim3(64), 0, s, static_cast<const u32x4*>(d),
+                         static_cast<u32x4*>(p));
+      const double us = us_since(t0);
+      CK(hipStreamSynchronize(s));
+      if (i >= 50) t.push_back(us);
+    }
+    report("copy, call only", t);
+    t.clear();
+  }
   {
     static BigArgs ba;
     ba.n = 7;
@@ -218,6 +278,40 @@ int main(int argc, char** argv) {
   }
   if (arm != nullptr) report("encode kernel (dispatch)", t);
   t.clear();
+  // the probes, timed the same way (hipExtLaunchKernelGGL records e0 / e1 at
+  // the kernel's own dispatch); grids of 1 and of the batch's 1 KiB tiles
+  {
+    const uint32_t tiles = (uint32_t)std::min<size_t>(S * m * bs / 1024, S * k * bs / 1024);
+    const u32x4* src = static_cast<const u32x4*>(d);
+    u32x4* dst = static_cast<u32x4*>(p);
+    auto timed = [&](const char* name, auto launch) -> int {
+      for (int i = 0; i < 500; ++i) {
+        launch();
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(ms * 1e3);
+      }
+      report(name, t);
+      t.clear();
+      return 0;
+    };
+    char nm[64];
+    for (uint32_t grid : {1u, tiles}) {
+      std::snprintf(nm, sizeof nm, "empty x%u (dispatch)", grid);
+      if (timed(nm, [&] { hipExtLaunchKernelGGL(empty_kernel, dim3(grid), dim3(64), 0, s, e0, e1, 0); }))
+        return 1;
+      std::snprintf(nm, sizeof nm, "load x%u (dispatch)", grid);
+      if (timed(nm, [&] { hipExtLaunchKernelGGL(load_probe, dim3(grid), dim3(64), 0, s, e0, e1, 0, src, dst, 0x12345u); }))
+        return 1;
+      std::snprintf(nm, sizeof nm, "store x%u (dispatch)", grid);
+      if (timed(nm, [&] { hipExtLaunchKernelGGL(store_probe, dim3(grid), dim3(64), 0, s, e0, e1, 0, dst, 7u); }))
+        return 1;
+      std::snprintf(nm, sizeof nm, "copy x%u (dispatch)", grid);
+      if (timed(nm, [&] { hipExtLaunchKernelGGL(copy_probe, dim3(grid), dim3(64), 0, s, e0, e1, 0, src, dst); }))
+        return 1;
+    }
+  }
   // decode: `lost` data blocks per stripe; with one, (7c) mod k (bench.py's
   // pattern), with more, block j + m * ((7c) mod (k/m)) of classes j < lost
   uint8_t* h_bm;
