@@ -34,7 +34,7 @@ thread_local int g_max_grid = 0;
 thread_local int g_nt = 0;
 thread_local int g_threads = 0;
 thread_local int g_occupancy = 0;      // waves per SIMD, 0 = automatic
-thread_local int g_decode_tiling = 0;  // 0 auto, 1 stripe, 2 class, 3 list
+thread_local int g_decode_tiling = 0;  // 0 auto, 1 stripe, 2 class, 3 list, 4 mask
 thread_local int g_arg_cap_used = 0;   // xec_decode_arg_capacity_used
 thread_local int g_tiling_used = 0;    // xec_decode_tiling_used: this thread's last xec_decode
 thread_local int g_rotation = 0;       // xec_set_rotation: 0 automatic, -1 none, > 0 tiles
@@ -110,7 +110,7 @@ bool use_class_tiles(uint64_t S, uint64_t m, uint64_t lost_data) {
   const int t = g_decode_tiling;
   if (m <= 1 || t == 1) return false;
   if (t == 2) return true;
-  return lost_data > S && 2 * lost_data >= S * m;  // automatic (0, or 3 without a list)
+  return lost_data > S && 2 * lost_data >= S * m;  // automatic (0, or 3 / 4 where n/a)
 }
 
 // ---- work-list staging -------------------------------------------------------
@@ -753,11 +753,33 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   // batches.  The list is built by a second, listing pass only
   // when it is used (the first pass costs ~1.1 ns per stripe).
   const int tiling = g_decode_tiling;
-  const bool listable =
-      (tiling == 0 || tiling == 3) && k <= kWorkItemMaxK && S <= kWorkItemMaxStripes;
+  const bool listable = (tiling == 0 || tiling == 3 || tiling == 4) && k <= kWorkItemMaxK &&
+                        S <= kWorkItemMaxStripes;
   const bool small = scan.lost_data <= xec::kArgItems;
   const bool sparse = scan.stripes_lost * kListStripesDen <= (uint64_t)S * kListStripesNum;
   const bool cls = use_class_tiles(S, m, scan.lost_data);
+  // A batch of at most kArgItems stripes (k <= 32) whose decode would upload
+  // something -- a list longer than the kernel arguments hold, or the bitmap
+  // for class / stripe tiles -- sends one loss mask per stripe in the kernel
+  // arguments instead and runs class tiles over them: nothing is copied, so a
+  // synchronous caller does not wait for a copy ahead of the kernel
+  // (decode_argmask_kernel; the reference's row 1126, 8 MiB (40/32) with 8
+  // losses, profiles/r06w).  Forced with xec_set_decode_tiling(4).
+  const bool arglist = listable && small && (tiling == 3 || sparse || !cls);
+  const bool maskable = !copy_first && S <= xec::kArgItems && k <= xec::kArgMaskMaxK;
+  if (maskable && (tiling == 4 || (tiling == 0 && !arglist))) {
+    uint32_t masks[xec::kArgItems];
+    xec_loss_masks(h_bitmap, S, k, m, masks);
+    // one reduction per tile, as encode: encode's residency table
+    xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+    ls.rot = decode_rotation(scan, m, bs);
+    const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
+    g_tiling_used = XEC_TILING_ARG_MASK;
+    g_arg_cap_used = (int)xec::arg_items_capacity(S);
+    const hipError_t le = xec::launch_decode(d_data, d_parity, nullptr, g, ls,
+                                             xec::kDecodeArgMaskTiles, stream, S, masks);
+    return le == hipSuccess ? XEC_SUCCESS : DEVERR(le);
+  }
   if (listable && (tiling == 3 || sparse || (!cls && small))) {
     // one reduction per tile, as encode: encode's residency table
     xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
@@ -1096,7 +1118,7 @@ xec_status xec_set_occupancy(int waves_per_simd) {
 }
 
 xec_status xec_set_decode_tiling(int tiling) {
-  if (tiling < 0 || tiling > 3) return XEC_INVALID_SIZE;
+  if (tiling < 0 || tiling > 4) return XEC_INVALID_SIZE;
   g_decode_tiling = tiling;
   return XEC_SUCCESS;
 }

@@ -45,3 +45,9 @@ xec_status xec_scan_bitmap(const uint8_t* h_bitmap, size_t S, size_t k, size_t m
 xec_status xec_scan_stripes(const uint8_t* h_bitmap, size_t S, size_t k, size_t m,
                             uint8_t* codes, uint32_t* items, uint64_t cap, uint64_t* n_items,
                             uint64_t* failures);
+
+// masks[c] = bit i set iff data byte i of stripe c's row is 0 (lost), for the
+// kernel-argument mask decode (xec_kernels.hip decode_argmask_kernel).
+// Requires k <= 32; the rows must already have passed xec_scan_bitmap (no
+// checks here).  Defined in xec_scan.cpp.
+void xec_loss_masks(const uint8_t* h_bitmap, size_t S, size_t k, size_t m, uint32_t* masks);

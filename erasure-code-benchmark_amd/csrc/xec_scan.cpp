@@ -352,6 +352,47 @@ xec_status xec_scan_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m, XecS
   return XEC_SUCCESS;
 }
 
+namespace {
+
+void loss_masks_scalar(const uint8_t* bm, size_t S, size_t k, size_t m, uint32_t* masks) {
+  const size_t row = k + m;
+  for (size_t c = 0; c < S; ++c) {
+    uint32_t mask = 0;
+    for (size_t i = 0; i < k; ++i) mask |= static_cast<uint32_t>(bm[c * row + i] == 0) << i;
+    masks[c] = mask;
+  }
+}
+
+#if defined(__x86_64__)
+// One 32-byte load per row covers its k <= 32 data bytes; the rows whose load
+// would pass the end of the bitmap go through a padded copy.
+__attribute__((target("avx2"))) void loss_masks_avx2(const uint8_t* bm, size_t S, size_t k,
+                                                     size_t m, uint32_t* masks) {
+  const size_t row = k + m, n = S * row;
+  const uint32_t data_mask = k == 32 ? ~0u : ((1u << k) - 1);
+  const __m256i zero = _mm256_setzero_si256();
+  size_t c = 0;
+  for (; c < S && c * row + 32 <= n; ++c) {
+    const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(bm + c * row));
+    masks[c] = static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(x, zero))) & data_mask;
+  }
+  if (c < S) loss_masks_scalar(bm + c * row, S - c, k, m, masks + c);
+}
+#endif
+
+}  // namespace
+
+void xec_loss_masks(const uint8_t* bm, size_t S, size_t k, size_t m, uint32_t* masks) {
+#if defined(__x86_64__)
+  static const bool fast = __builtin_cpu_supports("avx2");
+  if (fast) {
+    loss_masks_avx2(bm, S, k, m, masks);
+    return;
+  }
+#endif
+  loss_masks_scalar(bm, S, k, m, masks);
+}
+
 extern "C" xec_status xec_check_bitmap(const uint8_t* bm, size_t S, size_t k, size_t m,
                                        int* needs) {
   XecScan r;

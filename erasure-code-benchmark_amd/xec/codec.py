@@ -138,7 +138,8 @@ def set_occupancy(waves_per_simd: int = 0) -> Status:
 
 def set_decode_tiling(tiling: int = 0) -> Status:
     """xec_set_decode_tiling; 0 = automatic (default), 1 = stripe tiles, 2 = class tiles
-    (m > 1 only), 3 = work-list tiles where the list fits (identical results)."""
+    (m > 1 only), 3 = work-list tiles where the list fits, 4 = kernel-argument mask
+    tiles where they apply (S <= 1,024, k <= 32) (identical results)."""
     return Status(lib().xec_set_decode_tiling(tiling))
 
 
@@ -155,12 +156,14 @@ def set_validate_kernel(mode: int = 0) -> Status:
 
 #: xec_decode_tiling_used values (include/xec.h)
 DECODE_KERNELS = {1: "xec::decode_kernel", 2: "xec::decode_class_kernel",
-                  3: "xec::decode_list_kernel", 4: "xec::decode_arglist_kernel"}
+                  3: "xec::decode_list_kernel", 4: "xec::decode_arglist_kernel",
+                  5: "xec::decode_argmask_kernel"}
 
 
 def decode_tiling_used() -> int:
     """xec_decode_tiling_used: the tiling this thread's last xec_decode launched
-    (0 none, 1 stripe, 2 class, 3 device list, 4 kernel-argument list)."""
+    (0 none, 1 stripe, 2 class, 3 device list, 4 kernel-argument list,
+    5 kernel-argument masks)."""
     return int(lib().xec_decode_tiling_used())
 
 

@@ -83,7 +83,9 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * waits only for that copy before the decode kernel.  When `stream` is idle
  * (a synchronous caller) the copy goes into d_bitmap on `stream` itself, which
  * then starts at once without a cross-stream hand-off.  Up to 1,024 list
- * entries travel in the kernel arguments instead, and then nothing is copied.
+ * entries travel in the kernel arguments instead, and then nothing is copied;
+ * so do batches of at most 1,024 stripes with k <= 32 that would otherwise
+ * copy something (one loss mask per stripe, class tiles).
  * d_bitmap is scratch for the call.  Not
  * capturable: the host scan reads h_bitmap at call time, so a graph would
  * replay this call's losses -- on a stream being captured a call with blocks
@@ -247,10 +249,14 @@ xec_status xec_set_occupancy(int waves_per_simd);
  * when the batch lost more than one data block per stripe on average and at
  * least half of its S*m classes lost one, else stripe tiles -- one per
  * (stripe, chunk), rebuilding the stripe's lost blocks one after another.
+ * Batches of at most 1,024 stripes with k <= 32 that would upload the bitmap
+ * or a list send one loss mask per stripe in the kernel arguments instead
+ * (class tiles, nothing copied).
  * xec_decode_device (no host scan) uses stripe tiles.  1 = always stripe
  * tiles, 2 = always class tiles, 3 = work-list tiles where the list fits (else
- * the automatic bitmap choice).  Results are identical; only the speed
- * differs.  XEC_INVALID_SIZE outside 0..3. */
+ * the automatic bitmap choice), 4 = kernel-argument mask tiles where they
+ * apply (else automatic).  Results are identical; only the speed differs.
+ * XEC_INVALID_SIZE outside 0..4. */
 xec_status xec_set_decode_tiling(int tiling);
 
 /* Tuning / diagnostics (no reference counterpart): kernel shape of
@@ -295,12 +301,15 @@ enum {
   XEC_TILING_STRIPE = 1,   /* decode_kernel: (stripe, chunk) tiles over the bitmap */
   XEC_TILING_CLASS = 2,    /* decode_class_kernel: (stripe, class, chunk) tiles */
   XEC_TILING_LIST = 3,     /* decode_list_kernel: (lost block, chunk), list in d_bitmap */
-  XEC_TILING_ARG_LIST = 4  /* decode_arglist_kernel: the same, list in the kernel arguments */
+  XEC_TILING_ARG_LIST = 4, /* decode_arglist_kernel: the same, list in the kernel arguments */
+  XEC_TILING_ARG_MASK = 5  /* decode_argmask_kernel: class tiles, one loss mask per stripe
+                              in the kernel arguments (S <= 1,024, k <= 32) */
 };
 int xec_decode_tiling_used(void);
 /* With XEC_TILING_ARG_LIST: how many entries the kernel-argument list of that
  * launch could hold -- 64, 256 or 1024, the smallest capacity that holds the
- * list, so a short list ships short kernel arguments; 0 for any other tiling. */
+ * list, so a short list ships short kernel arguments; with XEC_TILING_ARG_MASK
+ * the same for its S stripe masks; 0 for any other tiling. */
 int xec_decode_arg_capacity_used(void);
 
 /* Diagnostics / measurement: the calling thread's NEXT xec_encode, xec_decode,

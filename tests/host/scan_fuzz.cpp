@@ -4,8 +4,8 @@
 // 64-byte windows) is reported.  Verdicts are compared with a direct
 // restatement of require_recovery / is_recoverable (xorec_utils.hpp:144-175);
 // xec_scan_bitmap's lost-data-block count and its work list (every zero data
-// byte as c << 8 | i, in batch order, truncated at the capacity) are checked
-// against a direct enumeration.
+// byte as c << 8 | i, in batch order, truncated at the capacity) and
+// xec_loss_masks' per-stripe masks are checked against a direct enumeration.
 //   g++ -std=c++17 -O1 -g -fsanitize=address,undefined -I include \
 //       tests/host/scan_fuzz.cpp erasure-code-benchmark_amd/csrc/xec_scan.cpp
 #include <algorithm>
@@ -86,6 +86,19 @@ int main() {
       if (items_ok && sp.listed < cap) ++spec_stops;
     }
     delete[] items;
+    // per-stripe loss masks (xec_loss_masks, k <= 32), read from the exact-size
+    // buffer so that a read past the bitmap's end shows under ASan
+    bool masks_ok = true;
+    if (k <= 32) {
+      std::vector<uint32_t> masks(S ? S : 1, 0xA5A5A5A5u);
+      xec_loss_masks(bm, S, k, m, masks.data());
+      for (size_t c = 0; masks_ok && c < S; ++c) {
+        uint32_t want_mask = 0;
+        for (size_t i = 0; i < k; ++i)
+          want_mask |= static_cast<uint32_t>(bm[c * (k + m) + i] == 0) << i;
+        masks_ok = masks[c] == want_mask;
+      }
+    }
     std::vector<uint8_t> bm_keep(bm, bm + n);
     delete[] bm;
     // per-stripe form: codes and the items of recoverable stripes only
@@ -111,7 +124,7 @@ int main() {
       for (size_t c = 0; ps_ok && c < S; ++c) ps_ok = codes[c] == codes_ref[c];
       for (size_t q = 0; ps_ok && q < ps_ref.size(); ++q) ps_ok = ps[q] == ps_ref[q];
     }
-    if (!items_ok || !stripes_ok || !ps_ok) {
+    if (!items_ok || !stripes_ok || !ps_ok || !masks_ok) {
       std::printf("WORK LIST MISMATCH trial %d k=%zu m=%zu S=%zu\n", trial, k, m, S);
       return 1;
     }

@@ -33,8 +33,9 @@ void fail(int t, int it, const char* what) {
 }
 
 // k=8+2, 4 KiB blocks: every stripe loses one data block in each class (so
-// class tiles are a valid forced choice and the automatic choice is class
-// tiles too -- a dense multi-erasure batch).
+// class tiles are a valid forced choice; the automatic choice for this dense
+// multi-erasure batch of 96 stripes is class tiles over kernel-argument loss
+// masks -- three threads, three different tilings).
 constexpr size_t kK = 8, kM = 2, kBs = 4096, kS = 96, kRow = kK + kM;
 
 void worker(int t, int tiling, int unroll, int threads, int occupancy, int validate_mode,
@@ -57,7 +58,8 @@ void worker(int t, int tiling, int unroll, int threads, int occupancy, int valid
     std::memset(hbm + c * kRow, 1, kRow);
     for (size_t j = 0; j < kM; ++j) hbm[c * kRow + j + kM * ((c + j + t) % (kK / kM))] = 0;
   }
-  const int want = tiling > 0 ? tiling : XEC_TILING_CLASS;  // auto: dense multi-erasure
+  // auto: dense multi-erasure over 96 stripes -> the kernel-argument masks
+  const int want = tiling > 0 ? tiling : XEC_TILING_ARG_MASK;
   for (int it = 0; it < iterations; ++it) {
     if (xec_fill_splitmix64(d, kS, kK * kBs, 1000 * t + it, s) ||
         xec_encode(d, p, kS, kBs, kK, kM, s) ||

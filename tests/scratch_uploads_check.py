@@ -35,7 +35,7 @@ def main():
     cases = [
         (2048, 4, 1, 256, "every", 0, False),    # stripe tiles: bitmap via the scratch
         (18432, 4, 1, 256, "sparse", 0, False),  # 2,048-entry list via the scratch
-        (64, 16, 2, 4096, "every_class", 0, False),  # class tiles
+        (1040, 16, 2, 1024, "every_class", 0, False),  # class tiles (past the argument masks)
         (300, 16, 4, 1024, "every_class", 3, False),  # forced list of 1,200 > 1,024 entries
         (5000, 8, 8, 256, "every_class", 0, True),    # per-stripe: list in pieces
         (4096, 4, 2, 256, "every_class", 0, True),

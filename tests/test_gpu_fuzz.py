@@ -81,7 +81,7 @@ def test_block_larger_than_2gib(gpu):
     assert torch.equal(d[bs:], keep)
 
 
-DECODE_PATHS = ["auto", "stripe", "class", "list", "per_stripe", "device", "device_list"]
+DECODE_PATHS = ["auto", "stripe", "class", "list", "mask", "per_stripe", "device", "device_list"]
 
 
 def _recoverable_rows(bm, k, m):
@@ -99,8 +99,9 @@ def _decode_via(gpu, path, b, h_bm, d_bm):
     host sees (device paths: the device verdict)."""
     import torch
     S, k, m, bs = b.S, b.k, b.m, b.bs
-    if path in ("auto", "stripe", "class", "list"):
-        assert gpu.set_decode_tiling({"auto": 0, "stripe": 1, "class": 2, "list": 3}[path]) == 0
+    if path in ("auto", "stripe", "class", "list", "mask"):
+        tiling = {"auto": 0, "stripe": 1, "class": 2, "list": 3, "mask": 4}[path]
+        assert gpu.set_decode_tiling(tiling) == 0
         return int(gpu.decode(b.d, b.p, S, bs, k, m, h_bm, torch.empty_like(d_bm), b.stream))
     if path == "per_stripe":
         return int(gpu.decode_per_stripe(b.d, b.p, S, bs, k, m, h_bm, torch.empty_like(d_bm),

@@ -229,7 +229,7 @@ def test_encode_is_linear(gpu):
     assert torch.equal(torch.bitwise_xor(a.p, bb.p), pab)
 
 
-@pytest.mark.parametrize("tiling", [0, 1, 2, 3])
+@pytest.mark.parametrize("tiling", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("S,k,m,bs,pattern", [
     (64, 16, 2, 65536, "all"),      # every class lost a data block
     (48, 16, 8, 8192, "all"),       # 8 per stripe > the 6 list entries the scratch holds: bitmap
@@ -251,8 +251,8 @@ def test_encode_is_linear(gpu):
     (40, 32, 8, 4352, "devices"),   # two failed devices, in two classes
 ])
 def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
-    """xec_set_decode_tiling: stripe tiles, class tiles, work-list tiles and the
-    automatic choice rebuild the same bytes, whatever fraction of the classes
+    """xec_set_decode_tiling: stripe tiles, class tiles, work-list tiles,
+    kernel-argument masks and the automatic choice rebuild the same bytes, whatever fraction of the classes
     lost a block and however the losses spread over the stripes."""
     b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
     bm = np.ones((S, k + m), np.uint8)
@@ -355,7 +355,7 @@ def test_rotation_argument_range(gpu):
     assert gpu.set_rotation(0) == gpu.Status.SUCCESS
 
 
-@pytest.mark.parametrize("tiling", [1, 2, 3])
+@pytest.mark.parametrize("tiling", [1, 2, 3, 4])
 def test_golden_decode_fixtures_each_tiling(gpu, oracle, known_answers, tiling):
     assert gpu.set_decode_tiling(tiling) == gpu.Status.SUCCESS
     try:
@@ -392,8 +392,66 @@ def test_decode_arg_list_capacities_bit_exact(gpu, oracle, S, k, m, bs, lost):
         gpu.set_decode_tiling(0)
 
 
+@pytest.mark.parametrize("S,k,m,bs,per_stripe,expect", [
+    (256, 32, 8, 1024, 8, 5),    # the reference's row 1126: 8 MiB, (40/32), 8 lost per stripe
+    (256, 32, 8, 1024, 4, 5),    # 1,024 lost, dense: class tiles would upload the bitmap
+    (64, 16, 2, 4096, 2, 5),     # capacity 64, at its edge
+    (65, 16, 4, 1024, 4, 5),     # 256
+    (257, 8, 2, 512, 2, 5),      # 1024
+    (1024, 32, 4, 256, 4, 5),    # 1,024 stripes: the largest, k = 32
+    (600, 12, 4, 768, 3, 5),     # generic member count 3, 1,800 lost
+    (40, 32, 8, 4352, 8, 5),     # ragged tail tile
+    (1025, 8, 2, 256, 2, 2),     # one stripe past the argument masks: class tiles, uploaded
+    (64, 40, 8, 256, 8, 2),      # k > 32: class tiles, uploaded
+])
+def test_decode_arg_masks_bit_exact(gpu, oracle, S, k, m, bs, per_stripe, expect):
+    """Small batches (S <= 1,024, k <= 32) whose decode would upload the bitmap or
+    a list send one loss mask per stripe in the kernel arguments instead
+    (decode_argmask_kernel): bit-exact at every capacity and on both sides of the
+    limits, with the capacity reported as for the kernel-argument list."""
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    bm = np.ones((S, k + m), np.uint8)
+    rng = np.random.default_rng(S * 7 + k)
+    for c in range(S):
+        for j in rng.choice(m, size=per_stripe, replace=False):
+            bm[c, j + m * int(rng.integers(k // m))] = 0
+    erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+    assert gpu.decode_tiling_used() == expect
+    if expect == 5:
+        assert gpu.decode_arg_capacity_used() == (64 if S <= 64 else 256 if S <= 256 else 1024)
+
+
+@pytest.mark.parametrize("S,k,m,bs,kind", [
+    (100, 16, 1, 2048, "one"),     # m = 1: class tiles are stripe tiles
+    (96, 8, 2, 4096, "sparse"),    # sparse: the masks leave most tiles idle
+    (30, 12, 4, 1024, "parity"),   # lost parity beside lost data in the other classes
+])
+def test_decode_arg_masks_forced(gpu, oracle, S, k, m, bs, kind):
+    """xec_set_decode_tiling(4) takes the argument masks wherever they apply,
+    also where the automatic policy would pass a list."""
+    b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
+    rng = np.random.default_rng(S + m)
+    bm = np.ones((S, k + m), np.uint8)
+    for c in range(S):
+        if kind == "one" or (kind == "sparse" and c % 9 == 4):
+            bm[c, (7 * c) % k] = 0
+        else:
+            lost_par = int(rng.integers(m))
+            bm[c, k + lost_par] = 0
+            for j in range(m):
+                if j != lost_par:
+                    bm[c, j + m * int(rng.integers(k // m))] = 0
+    assert gpu.set_decode_tiling(4) == gpu.Status.SUCCESS
+    try:
+        erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
+        assert gpu.decode_tiling_used() == 5
+    finally:
+        gpu.set_decode_tiling(0)
+
+
 def test_decode_tiling_argument_range(gpu):
-    assert gpu.set_decode_tiling(4) == gpu.Status.INVALID_SIZE
+    assert gpu.set_decode_tiling(5) == gpu.Status.INVALID_SIZE
+    assert gpu.set_decode_tiling(4) == gpu.Status.SUCCESS
     assert gpu.set_decode_tiling(-1) == gpu.Status.INVALID_SIZE
     assert gpu.set_decode_tiling(0) == gpu.Status.SUCCESS
 
@@ -437,7 +495,8 @@ def _pattern(kind, S, k, m, rng):
 def _valid_tilings(bm, k, m):
     """Every tiling xec_decode may launch for this bitmap (include/xec.h): stripe
     tiles always; class tiles when m > 1; device-list tiles when the list fits
-    the S*(k+m)-byte scratch; kernel-argument list up to 1,024 blocks."""
+    the S*(k+m)-byte scratch; kernel-argument list up to 1,024 blocks;
+    kernel-argument masks up to 1,024 stripes with k <= 32."""
     lost = int((bm[:, :k] == 0).sum())
     S = bm.shape[0]
     v = {1}
@@ -447,6 +506,8 @@ def _valid_tilings(bm, k, m):
         v.add(3)
     if k <= 256 and S <= (1 << 24) and lost <= 1024:
         v.add(4)
+    if S <= 1024 and k <= 32:
+        v.add(5)
     return v
 
 

@@ -35,7 +35,8 @@ def _hip():
 def test_decode_on_short_lived_streams(gpu, rounds):
     import torch
     hip = _hip()
-    S, k, m, bs = 96, 8, 2, 65536
+    # more stripes than the kernel-argument masks cover (1,024), so the bitmap is uploaded
+    S, k, m, bs = 1040, 8, 2, 4096
     d = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
     p = torch.empty(S * m * bs, dtype=torch.uint8, device="cuda")
     cur = torch.cuda.current_stream()

@@ -25,7 +25,7 @@ def kernels() -> dict[str, dict]:
     subprocess.run(["make", "-C", str(PKG_DIR), "asm"], check=True, capture_output=True)
     text = ASM.read_text()
     out = {}
-    for m in re.finditer(r"^(_ZN3xec[12][0-9](encode|decode)_(?:class_|list_|arglist_|devlist_)?kernel\w+):.*?^\s*s_endpgm", text,
+    for m in re.finditer(r"^(_ZN3xec[12][0-9](encode|decode)_(?:class_|list_|arglist_|argmask_|devlist_)?kernel\w+):.*?^\s*s_endpgm", text,
                          re.S | re.M):
         out[m.group(1)] = {"body": m.group(0)}
     meta = re.findall(r"\.name:\s+(\S+)\n(.*?)\.vgpr_count:\s+(\d+)", text, re.S)
@@ -67,7 +67,7 @@ AUTO_OCCUPANCY = {4: 4, 8: 4, 16: 2, 32: 1}
 
 
 @pytest.mark.parametrize("kind", ["encode", "decode", "decode_class", "decode_list",
-                                  "decode_arglist", "decode_devlist"])
+                                  "decode_arglist", "decode_argmask", "decode_devlist"])
 @pytest.mark.parametrize("nm", sorted(AUTO_OCCUPANCY))
 def test_registers_admit_the_default_residency(kernels, kind, nm):
     hits = [k for n, k in kernels.items()

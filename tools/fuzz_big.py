@@ -33,7 +33,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "erasure-code-benchmark_amd"))
 
-PATHS = ["auto", "stripe", "class", "list", "per_stripe", "device", "device_list"]
+PATHS = ["auto", "stripe", "class", "list", "mask", "per_stripe", "device", "device_list"]
 
 
 def loss_pattern(np, rng, S, k, m, kind):
@@ -139,8 +139,8 @@ def main():
             erased = d.clone()
             erased_p = p.clone()
             scratch = torch.empty_like(d_bm)
-            if path in ("auto", "stripe", "class", "list"):
-                xec.set_decode_tiling({"auto": 0, "stripe": 1, "class": 2, "list": 3}[path])
+            if path in ("auto", "stripe", "class", "list", "mask"):
+                xec.set_decode_tiling({"auto": 0, "stripe": 1, "class": 2, "list": 3, "mask": 4}[path])
                 st = int(xec.decode(d, p, S, bs, k, m, h_bm, scratch, s))
                 xec.set_decode_tiling(0)
             elif path == "per_stripe":
