@@ -73,7 +73,8 @@ def main():
     b_enc, b_dec = algorithmic_bytes(S, k, m, bs)
     algo = {"xec::encode_kernel": b_enc, "xec::decode_kernel": b_dec * lost,
             "xec::decode_class_kernel": b_dec * lost, "xec::decode_list_kernel": b_dec * lost,
-            "xec::decode_arglist_kernel": b_dec * lost}
+            "xec::decode_arglist_kernel": b_dec * lost, "xec::decode_argmask_kernel": b_dec * lost,
+            "xec::decode_devlist_kernel": b_dec * lost}
 
     kernels = {}
     for name in sorted(set(fetch) & set(write)):
