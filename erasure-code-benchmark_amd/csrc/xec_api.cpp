@@ -761,23 +761,27 @@ static xec_status decode_impl(void* d_data, const void* d_parity, size_t S, size
   // A batch of at most kArgItems stripes (k <= 32) whose decode would upload
   // something -- a list longer than the kernel arguments hold, or the bitmap
   // for class / stripe tiles -- sends one loss mask per stripe in the kernel
-  // arguments instead and runs class tiles over them: nothing is copied, so a
-  // synchronous caller does not wait for a copy ahead of the kernel
-  // (decode_argmask_kernel; the reference's row 1126, 8 MiB (40/32) with 8
-  // losses, profiles/r06w).  Forced with xec_set_decode_tiling(4).
+  // arguments instead, over class tiles where the bitmap path would take them
+  // and stripe tiles otherwise: nothing is copied, so a synchronous caller
+  // does not wait for a copy ahead of the kernel (decode_argmask_kernel; the
+  // reference's row 1126, 8 MiB (40/32) with 8 losses, profiles/r06w).  Forced
+  // with xec_set_decode_tiling(4).
   const bool arglist = listable && small && (tiling == 3 || sparse || !cls);
   const bool maskable = !copy_first && S <= xec::kArgItems && k <= xec::kArgMaskMaxK;
   if (maskable && (tiling == 4 || (tiling == 0 && !arglist))) {
     uint32_t masks[xec::kArgItems];
     xec_loss_masks(h_bitmap, S, k, m, masks);
-    // one reduction per tile, as encode: encode's residency table
-    xec::LaunchShape ls = launch_shape(bs, auto_occupancy(k / m));
+    // class tiles: one reduction per tile, encode's residency table; stripe
+    // tiles: as the bitmap's stripe tiles
+    xec::LaunchShape ls = launch_shape(
+        bs, cls ? auto_occupancy(k / m) : decode_auto_occupancy(k / m, scan.lost_data, S));
     ls.rot = decode_rotation(scan, m, bs);
     const xec::Geometry g = xec::make_geometry(S, bs, k, m, ls);
-    g_tiling_used = XEC_TILING_ARG_MASK;
+    g_tiling_used = cls ? XEC_TILING_ARG_MASK : XEC_TILING_ARG_MASK_STRIPE;
     g_arg_cap_used = (int)xec::arg_items_capacity(S);
-    const hipError_t le = xec::launch_decode(d_data, d_parity, nullptr, g, ls,
-                                             xec::kDecodeArgMaskTiles, stream, S, masks);
+    const hipError_t le = xec::launch_decode(
+        d_data, d_parity, nullptr, g, ls,
+        cls ? xec::kDecodeArgMaskTiles : xec::kDecodeArgMaskStripeTiles, stream, S, masks);
     return le == hipSuccess ? XEC_SUCCESS : DEVERR(le);
   }
   if (listable && (tiling == 3 || sparse || (!cls && small))) {

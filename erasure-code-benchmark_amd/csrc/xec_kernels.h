@@ -115,7 +115,8 @@ hipError_t launch_encode(const void* d_data, void* d_parity, const Geometry& g,
 // (xec_internal.h xec_work_item), 4-byte aligned.
 // ArgList: list tiles over up to kArgItems work items passed by value in the
 // kernel arguments (h_items, host memory, read at launch): no copy at all.
-// ArgMask (below): class tiles, the losses by value in the kernel arguments.
+// ArgMask (below): class or stripe tiles, the losses by value in the kernel
+// arguments.
 constexpr int kDecodeStripeTiles = 0;
 constexpr int kDecodeClassTiles = 1;
 constexpr int kDecodeListTiles = 2;
@@ -129,8 +130,10 @@ constexpr uint32_t kDevListHeader = 1;  // u32 words before the first entry
 // ArgMask: class tiles (stripe, class, chunk) over S <= kArgItems stripes whose
 // losses travel in the kernel arguments as one mask per stripe (h_items[c] bit
 // i = data block i lost; k <= kArgMaskMaxK), n_items = S: a small decode with
-// any number of losses copies nothing to the device.
+// any number of losses copies nothing to the device.  ArgMaskStripe: the same
+// masks over stripe tiles (stripe, chunk).
 constexpr int kDecodeArgMaskTiles = 5;
+constexpr int kDecodeArgMaskStripeTiles = 6;
 constexpr uint64_t kArgMaskMaxK = 32;
 // The list travels in the kernel arguments, so a launch ships the whole array
 // whatever the list's length: each kernel that takes one is compiled for three

@@ -338,30 +338,43 @@ __global__ __launch_bounds__(T) void decode_arglist_kernel(uint8_t* data,
   }
 }
 
-// Argument-mask tiles (small batches: S <= 1,024 stripes, k <= 32): encode's
-// (stripe, class, chunk) tiles, as decode_class_kernel, but the losses travel
-// in the kernel arguments as one mask per stripe (bit i = data block i lost),
-// so a small decode copies nothing to the device whatever its number of
-// losses -- in a synchronous call the bitmap copy is a blit kernel of its own
-// ahead of the decode (3.7-4.4 us, profiles/r02o), as long as the reference's
-// 8 MiB kernels themselves.  A class holds at most one lost data block (the
-// host scan's recoverability check), so the tile's block is the lowest set
-// bit of the stripe's mask within the class's positions j, j+m, j+2m, ...
+// Argument-mask tiles (small batches: S <= 1,024 stripes, k <= 32): the losses
+// travel in the kernel arguments as one mask per stripe (bit i = data block i
+// lost), so a small decode copies nothing to the device whatever its number
+// of losses -- in a synchronous call the bitmap copy is a blit kernel of its
+// own ahead of the decode (3.7-4.4 us, profiles/r02o), as long as the
+// reference's 8 MiB kernels themselves.  Two tilings, as over the bitmap:
+//  * by_class: encode's (stripe, class, chunk) tiles, as decode_class_kernel.
+//    A class holds at most one lost data block (the host scan's
+//    recoverability check), so the tile's block is the lowest set bit of the
+//    stripe's mask within the class's positions j, j+m, j+2m, ...;
+//  * otherwise (stripe, chunk) tiles, as decode_kernel: the tile rebuilds
+//    every block its stripe's mask names, one class reduction after another
+//    (few losses per stripe: class tiles would mostly idle).
 template <int NM, int U, bool NT, int T, uint32_t CAP>
 __global__ __launch_bounds__(T) void decode_argmask_kernel(uint8_t* data,
                                                            const uint8_t* __restrict__ parity,
-                                                           Geometry g, ArgItems<CAP> masks) {
+                                                           Geometry g, uint32_t by_class,
+                                                           ArgItems<CAP> masks) {
   const uint32_t nm = NM > 0 ? (uint32_t)NM : (uint32_t)g.nm;
   const uint32_t m = (uint32_t)g.m;
   uint32_t class0 = 0;  // class 0's data positions: bits 0, m, 2m, ... (k <= 32)
   for (uint32_t r = 0; r < nm; ++r) class0 |= 1u << (r * m);
   for (uint64_t t0 = blockIdx.x; t0 < g.total_tiles; t0 += gridDim.x) {
     const uint64_t t = g.total_tiles - 1 - t0;  // from the end of the batch, as encode
-    const TileCoord tc = tile_coord(t, g);
-    const uint32_t lost = masks.v[tc.c] & (class0 << tc.j);
-    if (lost == 0) continue;
-    rebuild_item<NM, U, NT, T>(data, parity,
-                               ((uint32_t)tc.c << 8) | (uint32_t)__builtin_ctz(lost), tc.chunk, g);
+    if (by_class) {
+      const TileCoord tc = tile_coord(t, g);
+      const uint32_t lost = masks.v[tc.c] & (class0 << tc.j);
+      if (lost == 0) continue;
+      rebuild_item<NM, U, NT, T>(data, parity,
+                                 ((uint32_t)tc.c << 8) | (uint32_t)__builtin_ctz(lost), tc.chunk,
+                                 g);
+    } else {
+      const uint64_t c = t / g.tiles_per_block, chunk = t % g.tiles_per_block;
+      for (uint32_t lost = masks.v[c]; lost != 0; lost &= lost - 1)
+        rebuild_item<NM, U, NT, T>(data, parity,
+                                   ((uint32_t)c << 8) | (uint32_t)__builtin_ctz(lost), chunk, g);
+    }
   }
 }
 
@@ -560,17 +573,18 @@ hipError_t launch_decode_t(void* d, const void* p, const uint8_t* bm, const Geom
                       arg_items<1024>(al.items, al.n));
     }
   }
-  if (tiling == kDecodeArgMaskTiles) {
+  if (tiling == kDecodeArgMaskTiles || tiling == kDecodeArgMaskStripeTiles) {
+    const uint32_t by_class = tiling == kDecodeArgMaskTiles;
     switch (arg_items_capacity(al.n)) {
       case 64:
         return launch_codec(decode_argmask_kernel<NM, U, NT, T, 64>, grid, T, lds, s, dd, pp, g,
-                            arg_items<64>(al.items, al.n));
+                            by_class, arg_items<64>(al.items, al.n));
       case 256:
         return launch_codec(decode_argmask_kernel<NM, U, NT, T, 256>, grid, T, lds, s, dd, pp, g,
-                            arg_items<256>(al.items, al.n));
+                            by_class, arg_items<256>(al.items, al.n));
       default:
         return launch_codec(decode_argmask_kernel<NM, U, NT, T, 1024>, grid, T, lds, s, dd, pp, g,
-                            arg_items<1024>(al.items, al.n));
+                            by_class, arg_items<1024>(al.items, al.n));
     }
   }
   if (tiling == kDecodeListTiles)
@@ -644,17 +658,19 @@ hipError_t launch_decode(void* d_data, const void* d_parity, const uint8_t* d_bi
   // decode_arglist_kernel over h_items (<= kArgItems) passed by value;
   // device-built list: decode_devlist_kernel over the count d_bitmap[0]
   // holds (n_items = its upper bound, which only sizes the grid); argument
-  // masks: decode_argmask_kernel over class tiles, h_items = S stripe masks.
+  // masks: decode_argmask_kernel over class (or stripe) tiles, h_items = S
+  // stripe masks.
   Geometry g = g_class;
   if (tiling == kDecodeClassTiles && g.m <= 1) tiling = kDecodeStripeTiles;
-  if (tiling == kDecodeStripeTiles) g.total_tiles = g.S * g.tiles_per_block;
+  if (tiling == kDecodeStripeTiles || tiling == kDecodeArgMaskStripeTiles)
+    g.total_tiles = g.S * g.tiles_per_block;
   if (tiling == kDecodeListTiles || tiling == kDecodeArgListTiles ||
       tiling == kDecodeDevListTiles)
     g.total_tiles = n_items * g.tiles_per_block;
   if (g.total_tiles == 0) return hipSuccess;
   if (tiling == kDecodeArgListTiles && (n_items > kArgItems || h_items == nullptr))
     return hipErrorInvalidValue;
-  if (tiling == kDecodeArgMaskTiles &&
+  if ((tiling == kDecodeArgMaskTiles || tiling == kDecodeArgMaskStripeTiles) &&
       (n_items != g.S || n_items > kArgItems || g.k > kArgMaskMaxK || h_items == nullptr))
     return hipErrorInvalidValue;
   const ArgList a{h_items, n_items};

@@ -157,13 +157,13 @@ def set_validate_kernel(mode: int = 0) -> Status:
 #: xec_decode_tiling_used values (include/xec.h)
 DECODE_KERNELS = {1: "xec::decode_kernel", 2: "xec::decode_class_kernel",
                   3: "xec::decode_list_kernel", 4: "xec::decode_arglist_kernel",
-                  5: "xec::decode_argmask_kernel"}
+                  5: "xec::decode_argmask_kernel", 6: "xec::decode_argmask_kernel"}
 
 
 def decode_tiling_used() -> int:
     """xec_decode_tiling_used: the tiling this thread's last xec_decode launched
     (0 none, 1 stripe, 2 class, 3 device list, 4 kernel-argument list,
-    5 kernel-argument masks)."""
+    5 kernel-argument masks over class tiles, 6 the same over stripe tiles)."""
     return int(lib().xec_decode_tiling_used())
 
 

@@ -85,7 +85,7 @@ xec_status xec_encode(const void* d_data, void* d_parity, size_t S, size_t bs, s
  * then starts at once without a cross-stream hand-off.  Up to 1,024 list
  * entries travel in the kernel arguments instead, and then nothing is copied;
  * so do batches of at most 1,024 stripes with k <= 32 that would otherwise
- * copy something (one loss mask per stripe, class tiles).
+ * copy something (one loss mask per stripe).
  * d_bitmap is scratch for the call.  Not
  * capturable: the host scan reads h_bitmap at call time, so a graph would
  * replay this call's losses -- on a stream being captured a call with blocks
@@ -251,7 +251,7 @@ xec_status xec_set_occupancy(int waves_per_simd);
  * (stripe, chunk), rebuilding the stripe's lost blocks one after another.
  * Batches of at most 1,024 stripes with k <= 32 that would upload the bitmap
  * or a list send one loss mask per stripe in the kernel arguments instead
- * (class tiles, nothing copied).
+ * (class or stripe tiles by the same rule, nothing copied).
  * xec_decode_device (no host scan) uses stripe tiles.  1 = always stripe
  * tiles, 2 = always class tiles, 3 = work-list tiles where the list fits (else
  * the automatic bitmap choice), 4 = kernel-argument mask tiles where they
@@ -302,13 +302,14 @@ enum {
   XEC_TILING_CLASS = 2,    /* decode_class_kernel: (stripe, class, chunk) tiles */
   XEC_TILING_LIST = 3,     /* decode_list_kernel: (lost block, chunk), list in d_bitmap */
   XEC_TILING_ARG_LIST = 4, /* decode_arglist_kernel: the same, list in the kernel arguments */
-  XEC_TILING_ARG_MASK = 5  /* decode_argmask_kernel: class tiles, one loss mask per stripe
+  XEC_TILING_ARG_MASK = 5, /* decode_argmask_kernel: class tiles, one loss mask per stripe
                               in the kernel arguments (S <= 1,024, k <= 32) */
+  XEC_TILING_ARG_MASK_STRIPE = 6 /* the same masks over (stripe, chunk) tiles */
 };
 int xec_decode_tiling_used(void);
 /* With XEC_TILING_ARG_LIST: how many entries the kernel-argument list of that
  * launch could hold -- 64, 256 or 1024, the smallest capacity that holds the
- * list, so a short list ships short kernel arguments; with XEC_TILING_ARG_MASK
+ * list, so a short list ships short kernel arguments; with XEC_TILING_ARG_MASK(_STRIPE)
  * the same for its S stripe masks; 0 for any other tiling. */
 int xec_decode_arg_capacity_used(void);
 

@@ -401,13 +401,16 @@ def test_decode_arg_list_capacities_bit_exact(gpu, oracle, S, k, m, bs, lost):
     (1024, 32, 4, 256, 4, 5),    # 1,024 stripes: the largest, k = 32
     (600, 12, 4, 768, 3, 5),     # generic member count 3, 1,800 lost
     (40, 32, 8, 4352, 8, 5),     # ragged tail tile
+    (1000, 16, 8, 1024, 2, 6),   # 2,000 lost, a quarter of the classes: stripe tiles
+    (700, 24, 8, 512, 3, 6),     # generic member count 3 on stripe tiles
     (1025, 8, 2, 256, 2, 2),     # one stripe past the argument masks: class tiles, uploaded
     (64, 40, 8, 256, 8, 2),      # k > 32: class tiles, uploaded
 ])
 def test_decode_arg_masks_bit_exact(gpu, oracle, S, k, m, bs, per_stripe, expect):
     """Small batches (S <= 1,024, k <= 32) whose decode would upload the bitmap or
     a list send one loss mask per stripe in the kernel arguments instead
-    (decode_argmask_kernel): bit-exact at every capacity and on both sides of the
+    (decode_argmask_kernel, over class tiles (5) or stripe tiles (6) by the
+    bitmap path's rule): bit-exact at every capacity and on both sides of the
     limits, with the capacity reported as for the kernel-argument list."""
     b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
     bm = np.ones((S, k + m), np.uint8)
@@ -417,18 +420,19 @@ def test_decode_arg_masks_bit_exact(gpu, oracle, S, k, m, bs, per_stripe, expect
             bm[c, j + m * int(rng.integers(k // m))] = 0
     erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
     assert gpu.decode_tiling_used() == expect
-    if expect == 5:
+    if expect in (5, 6):
         assert gpu.decode_arg_capacity_used() == (64 if S <= 64 else 256 if S <= 256 else 1024)
 
 
-@pytest.mark.parametrize("S,k,m,bs,kind", [
-    (100, 16, 1, 2048, "one"),     # m = 1: class tiles are stripe tiles
-    (96, 8, 2, 4096, "sparse"),    # sparse: the masks leave most tiles idle
-    (30, 12, 4, 1024, "parity"),   # lost parity beside lost data in the other classes
+@pytest.mark.parametrize("S,k,m,bs,kind,expect", [
+    (100, 16, 1, 2048, "one", 6),      # m = 1: stripe tiles
+    (96, 8, 2, 4096, "sparse", 6),     # sparse: stripe tiles, most of them idle
+    (30, 12, 4, 1024, "parity", 5),    # lost parity beside lost data in the other classes
 ])
-def test_decode_arg_masks_forced(gpu, oracle, S, k, m, bs, kind):
+def test_decode_arg_masks_forced(gpu, oracle, S, k, m, bs, kind, expect):
     """xec_set_decode_tiling(4) takes the argument masks wherever they apply,
-    also where the automatic policy would pass a list."""
+    also where the automatic policy would pass a list; class tiles or stripe
+    tiles by the bitmap path's rule."""
     b, ref_d, ref_p = encode_and_check(gpu, oracle, S, k, m, bs)
     rng = np.random.default_rng(S + m)
     bm = np.ones((S, k + m), np.uint8)
@@ -444,7 +448,7 @@ def test_decode_arg_masks_forced(gpu, oracle, S, k, m, bs, kind):
     assert gpu.set_decode_tiling(4) == gpu.Status.SUCCESS
     try:
         erase_decode_check(gpu, b, ref_d, ref_p, bm.reshape(-1))
-        assert gpu.decode_tiling_used() == 5
+        assert gpu.decode_tiling_used() == expect
     finally:
         gpu.set_decode_tiling(0)
 
@@ -507,7 +511,7 @@ def _valid_tilings(bm, k, m):
     if k <= 256 and S <= (1 << 24) and lost <= 1024:
         v.add(4)
     if S <= 1024 and k <= 32:
-        v.add(5)
+        v |= {5, 6}
     return v
 
 
