@@ -302,6 +302,8 @@ def test_decode_tilings_bit_exact(gpu, oracle, tiling, S, k, m, bs, pattern):
     (40, 32, 8, 4352, "all", 0),         # ragged tail chunk moved by the rotation
     (33, 8, 2, 2048 + 768, "one", 3),    # ragged, device-memory list
     (9, 10, 5, 768, "all", 0),           # generic member count, one ragged chunk
+    (16, 16, 2, 1 << 20, "device", 4),   # one failed device over stripe tiles of loss masks
+    (33, 8, 2, 2048 + 768, "one", 4),    # ragged, loss masks
 ])
 def test_rotation_bit_exact(gpu, oracle, rot, S, k, m, bs, pattern, tiling):
     """xec_set_rotation: every column rotation, automatic (0) and none (-1)
